@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""TCSC sparse-ternary GEMM benchmark (BASELINE.json metric) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+A "step" is one pass of the hot path over one batch: one launch of the gfx950
+gather kernel computing Y = PReLU(X*W + b) for this rank's output columns,
+inputs already resident in HBM.  N=1 runs BASELINE configs[3] (cfg4: M=4096,
+K=N=16384, 98 % sparse, PReLU) -- the configuration the north star's target
+is quoted on.  With N ranks each GPU owns one column block:
+  --scaling weak   (default) every rank owns a full 16384-column block of a
+                   N*16384-column W (per-GPU work fixed as N grows);
+  --scaling strong the cfg4 matrix itself is split into N column blocks.
+There is no collective on the data path; the only collectives are the
+timing barrier and the max-over-ranks of the elapsed time.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with
+`roofline` for the gather kernel (algorithmic bytes per launch / average
+launch time measured with HIP events on the launch stream) and
+`cpu_baseline` (the oracle's restatement of tcsc_sgemm_prelu_basic timed on
+this host's cores on a bounded sample of the same workload).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "sparse-matrix-multiplication-benchmark_amd")
+sys.path.insert(0, PKG)
+
+METRIC = "TCSC SpMM: effective G-add-ops/s + achieved HBM GB/s vs roofline, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# LDS gather roof: ds_read_b64/b128 move 256 B/clk/CU = 64 fp32 per clk per CU
+LDS_GATHER_PEAK = 64 * 256 * 2.4e9  # gathered fp32 values / s
+VALU_ADD_PEAK = 128 * 256 * 2.4e9  # fp32 adds / s (4 SIMD32 per CU)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", type=int, default=4)
+    p.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    p.add_argument("--variant", default=None, help="override the config's variant")
+    p.add_argument("--shard-of", type=int, default=0,
+                   help="time only rank 0's block of an S-way strong split (per-GPU view of S GPUs)")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import tcsc_amd
+    from tcsc_amd import workloads
+    from tcsc_amd.shard import column_range, rank_env
+
+    rank, local_rank, world = rank_env()
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 needs one process per GPU: launch with torchrun --nproc-per-node N")
+    distributed = world > 1
+    if distributed:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    tcsc_amd.require_gpu()
+
+    cfg = workloads.CONFIGS[args.config]
+    variant = args.variant or cfg.variant
+    # this rank's column block
+    if args.scaling == "weak":
+        c0, c1, seed_off = 0, cfg.N, rank
+    else:
+        c0, c1 = column_range(cfg.N, world, rank)
+        seed_off = 0
+    if args.shard_of > 1:
+        c0, c1 = column_range(cfg.N, args.shard_of, 0)
+    ncols = c1 - c0
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    # ---- setup (not timed): synthetic inputs + device TCSC + plan --------
+    inp = workloads.make_device_inputs(cfg, c0, c1, dev, seed_offset=seed_off)
+    csp = torch.empty(ncols + 1, dtype=torch.int32, device=dev)
+    csn = torch.empty(ncols + 1, dtype=torch.int32, device=dev)
+    npos, nneg = tcsc_amd.gpu_from_dense(inp["Wd"], cfg.K, ncols, csp, csn, stream=sh)
+    rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
+    rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
+    tcsc_amd.gpu_from_dense(inp["Wd"], cfg.K, ncols, csp, csn, rip, rin, stream=sh)
+    del inp["Wd"]
+    plan = tcsc_amd.Plan.from_device(cfg.K, ncols, csp, csn, rip, rin, 0, ncols, local_rank, sh)
+    nnz = npos + nneg
+    X, B = inp["X"], inp["B"]
+    Y = torch.empty((cfg.M, ncols), device=dev, dtype=torch.float32)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        plan.sgemm(X, B, Y, cfg.M, ncols, variant, 0.2, sh)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_s = ev0.elapsed_time(ev1) / 1e3 / max(args.steps, 1)
+
+    ops_rank = workloads.add_ops(cfg.M, nnz, ncols) * args.steps
+    stats = torch.tensor([elapsed, float(ops_rank)], dtype=torch.float64, device=dev)
+    if distributed:
+        t_max = stats[:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        ops_tot = stats[1:].clone()
+        dist.all_reduce(ops_tot, op=dist.ReduceOp.SUM)
+        elapsed_max, ops_total = float(t_max.item()), float(ops_tot.item())
+    else:
+        elapsed_max, ops_total = elapsed, float(ops_rank)
+
+    if rank == 0:
+        algo_bytes = workloads.algorithmic_bytes(cfg.M, cfg.K, ncols, nnz)
+        achieved = algo_bytes / kernel_s / 1e9
+        adds_per_launch = workloads.add_ops(cfg.M, nnz, ncols)
+        traffic = None
+        try:
+            with open(args.traffic) as f:
+                t = json.load(f)
+            key = f"cfg{cfg.idx}:{variant}:{ncols}"
+            if key in t:
+                traffic = t[key]["hbm_bytes_per_launch"]
+        except (OSError, ValueError, KeyError):
+            traffic = None
+        out = {
+            "metric": METRIC,
+            "value": ops_total / elapsed_max / 1e9,
+            "unit": "G-add-ops/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": args.scaling,
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (X,B ~ U[-1,1), W iid ternary; seeded torch generators)",
+            "config": {
+                "workload": f"{cfg.name}: {cfg.describe()}",
+                "M": cfg.M, "K": cfg.K, "N": cfg.N, "sparsity": cfg.sparsity, "variant": variant,
+                "columns_per_gpu": ncols, "nnz_per_gpu": nnz,
+                "parallelism": f"column-shard x{world} ({args.scaling}), no collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "k_tcsc_gather",
+                "algorithmic_bytes_per_launch": algo_bytes,
+                "kernel_ms": kernel_s * 1e3,
+                "lds_gather_frac": (cfg.M * nnz / kernel_s) / LDS_GATHER_PEAK,
+                "valu_add_frac": (adds_per_launch / kernel_s) / VALU_ADD_PEAK,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, cfg, variant, X, B, csp, csn, rip[:npos], rin[:nneg])
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, cfg, variant, X, B, csp, csn, rip, rin):
+    """Oracle (C restatement of tcsc_sgemm_prelu_basic, 1 core; and the
+    OpenMP sparseGEMM_PReLU restatement on all cores) on row blocks of the
+    same workload until ~cpu_seconds of CPU work are spent."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
+    import pyoracle
+
+    o = pyoracle.load_oracle()
+    ncols = csp.numel() - 1
+    W = pyoracle.TCSC(cfg.K, ncols, csp.cpu().numpy(), csn.cpu().numpy(), rip.cpu().numpy(), rin.cpu().numpy())
+    Bh = B.cpu().numpy()
+    nnz = W.nnz
+    # 1 core, scalar port of the reference's loop (tcsc.c:143-165)
+    rows_per_block = 16
+    done, t0 = 0, time.perf_counter()
+    budget = args.cpu_seconds
+    while done < cfg.M:
+        r1 = min(cfg.M, done + rows_per_block)
+        Xs = X[done:r1].cpu().numpy()
+        o.sgemm(variant if variant in pyoracle.VARIANTS else "prelu_basic", Xs, W, Bh, 0.2)
+        done = r1
+        if time.perf_counter() - t0 > budget:
+            break
+    t1 = time.perf_counter() - t0
+    v1 = (done * nnz + done * ncols) / t1 / 1e9
+    # all host cores (OpenMP, SparseGEMM.h:151-168 order)
+    threads = min(os.cpu_count() or 1, 16)
+    rows = min(cfg.M, max(64, done * threads))
+    Xs = X[:rows].cpu().numpy()
+    t2 = time.perf_counter()
+    o.sparse_gemm_omp(Xs, W, Bh, prelu=True, a=0.2, threads=threads)
+    t2 = time.perf_counter() - t2
+    vomp = (rows * nnz + rows * ncols) / t2 / 1e9
+    return {
+        "value": v1,
+        "unit": "G-add-ops/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{cfg.name}: first {done} of {cfg.M} rows x all {ncols} columns, {variant} "
+                  f"(oracle/tcsc_oracle.c, gcc -O2), {t1:.1f} s",
+        "omp_value": vomp,
+        "omp_cores": threads,
+        "omp_sample": f"first {rows} rows, oracle_sparse_gemm_omp ({threads} threads), {t2:.1f} s",
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,127 @@
+/*
+ * tcsc_gpu.h -- device-pointer extension of the TCSC drop-in API.
+ *
+ * The reference's API (sparse/tcsc.h:19-48) only takes host pointers and is
+ * synchronous, so a call through it always pays PCIe transfers.  These entry
+ * points expose the same computation on device-resident buffers, on a caller
+ * supplied HIP stream, so that kernel-only throughput can be measured and so
+ * that one process per GPU (torch.distributed ranks, MPI ranks, ...) can run
+ * its own column shard.  Plain C ABI: no HIP or torch types in the
+ * signatures; streams are passed as `void*` (a hipStream_t, NULL = the
+ * device's null stream).
+ *
+ * A plan is the device-side image of (a column range of) one tcsc_t,
+ * re-laid out for the gfx950 gather kernel ("Data layout in
+ * HBM").  Building a plan is the only place W's index arrays cross PCIe.
+ */
+#ifndef TCSC_AMD_TCSC_GPU_H
+#define TCSC_AMD_TCSC_GPU_H
+
+#include <stddef.h>
+#include "sparse/tcsc.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Which reference entry point a launch stands in for.  The GPU computes all
+ * of them with one kernel family; the variant only selects the epilogue
+ * (PReLU or not).  See DESIGN.md "Numerics" for the summation order. */
+enum tcsc_variant {
+    TCSC_VARIANT_BASIC = 0,            /* tcsc_sgemm_basic                    tcsc.c:69  */
+    TCSC_VARIANT_OPTIMIZED = 1,        /* tcsc_sgemm_optimized                tcsc.c:101 */
+    TCSC_VARIANT_PRELU_BASIC = 2,      /* tcsc_sgemm_prelu_basic              tcsc.c:143 */
+    TCSC_VARIANT_PRELU_SEPARATE = 3,   /* tcsc_sgemm_prelu_optimized_separate tcsc.c:179 */
+    TCSC_VARIANT_PRELU_ONTHEGO = 4     /* tcsc_sgemm_prelu_optimized_onthego  tcsc.c:231 */
+};
+
+/* Status codes (0 = success).  HIP errors are passed through as
+ * TCSC_E_HIP; the message is in tcsc_gpu_last_error(). */
+enum tcsc_status {
+    TCSC_OK = 0,
+    TCSC_E_ARG = 1,      /* bad argument (shape mismatch, NULL, range)   */
+    TCSC_E_HIP = 2,      /* a HIP runtime call failed                     */
+    TCSC_E_NOMEM = 3,    /* host or device allocation failed              */
+    TCSC_E_NODEV = 4     /* no usable gfx950 device                       */
+};
+
+typedef struct tcsc_gpu_plan tcsc_gpu_plan;
+
+typedef struct {
+    int device;          /* HIP device ordinal the plan lives on          */
+    int rows;            /* K                                             */
+    int cols;            /* columns in this plan (col_end - col_begin)    */
+    int col_begin;       /* first column of W covered                     */
+    long long nnz;       /* +1 and -1 entries in the covered columns      */
+    long long n_pos, n_neg;
+    int chunk_k;         /* K rows per LDS chunk used by the kernel       */
+    int n_chunks;        /* ceil(K / chunk_k)                             */
+    size_t device_bytes; /* HBM held by the plan                          */
+} tcsc_gpu_plan_info;
+
+/* Number of HIP devices visible (0 when there is no GPU). */
+int tcsc_gpu_device_count(void);
+
+/* Upload columns [col_begin, col_end) of W to `device` and build the plan.
+ * W is read on the host; `stream` orders the uploads and the build kernels.
+ * The call returns after the plan is complete (it synchronises `stream`). */
+int tcsc_gpu_plan_create(const tcsc_t *W, int col_begin, int col_end,
+                         int device, void *stream, tcsc_gpu_plan **out);
+
+/* Same, from raw TCSC arrays that already live on `device` (the layout of
+ * tcsc_t: col_start_* have cols+1 entries, absolute offsets).  Nothing
+ * crosses PCIe. */
+int tcsc_gpu_plan_create_device(int rows, int cols,
+                                const int *d_col_start_pos,
+                                const int *d_col_start_neg,
+                                const int *d_row_index_pos,
+                                const int *d_row_index_neg,
+                                int col_begin, int col_end, int device,
+                                void *stream, tcsc_gpu_plan **out);
+
+int tcsc_gpu_plan_get_info(const tcsc_gpu_plan *plan, tcsc_gpu_plan_info *info);
+void tcsc_gpu_plan_destroy(tcsc_gpu_plan *plan);
+
+/* Y[m, j] = act(B[j] + sum_{k in P(j)} X[m,k] - sum_{k in Q(j)} X[m,k])
+ * for m < M and the plan's columns j < cols.
+ *   dX : M x K row-major device array (K = plan rows), 4-byte aligned
+ *   dB : `cols` floats (the plan's slice of the bias)
+ *   dY : M rows with pitch `ldy` floats (ldy >= cols); columns beyond
+ *        `cols` are not touched
+ *   act: PReLU(v) = (v < 0 ? a*v : v) for the PRELU variants, identity
+ *        otherwise.
+ * Asynchronous on `stream`; no allocation, no synchronisation (safe to
+ * capture in a hipGraph). */
+int tcsc_gpu_sgemm(const tcsc_gpu_plan *plan, const float *dX, const float *dB,
+                   float *dY, int M, int ldy, int variant, float a,
+                   void *stream);
+
+/* Device-side tcsc_from_dense: dense K x N row-major float matrix on the
+ * device -> TCSC arrays on the device, bit-exact with the reference builder
+ * (tcsc.c:6-66).  Two calls: first with the four output pointers NULL to
+ * get n_pos / n_neg (col_start arrays are still written), then with the
+ * index arrays allocated.  Synchronises `stream`. */
+int tcsc_gpu_from_dense(const float *d_dense, int rows, int cols,
+                        int *d_col_start_pos, int *d_col_start_neg,
+                        int *d_row_index_pos, int *d_row_index_neg,
+                        int *n_pos, int *n_neg, void *stream);
+
+/* Message for the last failing call on this thread ("" if none). */
+const char *tcsc_gpu_last_error(void);
+
+/* Drop every device copy the host-pointer API cached (all tcsc_t's). */
+void tcsc_gpu_cache_clear(void);
+
+/* Number of GPUs the host-pointer API (sparse/tcsc.h) spreads columns over:
+ * min(visible devices, $TCSC_NUM_GPUS if set).  `tcsc_gpu_set_num_shards`
+ * overrides the count of column blocks (blocks are dealt round-robin over
+ * the devices; >devices is allowed and is how the multi-block path is
+ * exercised on a single GPU). 0 restores the default. */
+int tcsc_gpu_num_shards(void);
+void tcsc_gpu_set_num_shards(int shards);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TCSC_AMD_TCSC_GPU_H */

@@ -1,0 +1,598 @@
+// tcsc_api.cpp -- the C ABI of libtcsc_amd.so.
+//
+//  * include/tcsc_gpu.h : device-pointer API (plans, async launches).
+//  * include/sparse/tcsc.h : the reference's host-pointer API
+//    (sparse/tcsc.h:19-48), implemented on top of the device API:
+//    per-tcsc_t plan cache on every GPU used, per-call H2D of X and B, one
+//    launch per column block, D2H of each block straight into Y's columns.
+//
+// Error policy: the reference's kernels return void and cannot fail.  Here a
+// HIP failure is recorded (tcsc_gpu_last_error()), printed on stderr and --
+// unless TCSC_ON_ERROR=continue -- aborts, because silently leaving Y
+// unwritten would be worse than the reference's behaviour.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/sparse/tcsc.h"
+#include "../../include/tcsc_gpu.h"
+#include "tcsc_internal.h"
+
+struct tcsc_gpu_plan {
+    int device = 0;
+    int rows = 0, cols = 0, col_begin = 0;
+    long long n_pos = 0, n_neg = 0;
+    int chunk_k = tcsc::kChunkK, n_chunks = 0;
+    int* ent = nullptr;
+    int* cptr = nullptr;
+    size_t bytes = 0;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+void set_error(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    set_error("%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+    return TCSC_E_HIP;
+}
+
+#define HIP_TRY(call)                                      \
+    do {                                                   \
+        hipError_t e_ = (call);                            \
+        if (e_ != hipSuccess) return hip_fail(e_, #call);  \
+    } while (0)
+
+// RAII device allocation
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t alloc(size_t bytes) {
+        return hipMalloc(&p, bytes ? bytes : 4);
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
+int device_count_raw() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+// Build a plan from device-resident TCSC arrays (absolute offsets).
+int build_plan(int rows, int col_begin, int ncols, long long n_pos, long long n_neg, const int* csp,
+               const int* csn, const int* rip, const int* rin, int device, hipStream_t st,
+               tcsc_gpu_plan** out) {
+    auto plan = std::make_unique<tcsc_gpu_plan>();
+    plan->device = device;
+    plan->rows = rows;
+    plan->cols = ncols;
+    plan->col_begin = col_begin;
+    plan->n_pos = n_pos;
+    plan->n_neg = n_neg;
+    plan->chunk_k = tcsc::kChunkK;
+    plan->n_chunks = rows > 0 ? (rows + plan->chunk_k - 1) / plan->chunk_k : 0;
+    const long long nnz = n_pos + n_neg;
+    const long long nb = (long long)plan->n_chunks * ncols;
+    if (nnz > 0x7fffffffLL - tcsc::kEntPad || nb + 1 > 0x7fffffffLL) {
+        set_error("plan too large: nnz=%lld buckets=%lld", nnz, nb);
+        return TCSC_E_ARG;
+    }
+    HIP_TRY(hipMalloc(&plan->ent, (size_t)(nnz + tcsc::kEntPad) * sizeof(int)));
+    HIP_TRY(hipMalloc(&plan->cptr, (size_t)(nb + 1) * sizeof(int)));
+    plan->bytes = (size_t)(nnz + tcsc::kEntPad + nb + 1) * sizeof(int);
+    HIP_TRY(hipMemsetAsync(plan->ent, 0, (size_t)(nnz + tcsc::kEntPad) * sizeof(int), st));
+    if (nb == 0) {
+        HIP_TRY(hipMemsetAsync(plan->cptr, 0, sizeof(int), st));
+    } else {
+        tcsc::PlanDev in;
+        in.rows = rows;
+        in.ncols = ncols;
+        in.col_begin = col_begin;
+        in.n_pos = n_pos;
+        in.n_neg = n_neg;
+        in.csp = csp;
+        in.csn = csn;
+        in.rip = rip;
+        in.rin = rin;
+        tcsc::PlanOut po;
+        po.chunk_k = plan->chunk_k;
+        po.n_chunks = plan->n_chunks;
+        po.ent = plan->ent;
+        po.cptr = plan->cptr;
+        DevBuf lbp, lbn, cnt, tmp;
+        const size_t nbnd = (size_t)(plan->n_chunks + 1) * ncols;
+        HIP_TRY(lbp.alloc(nbnd * sizeof(int)));
+        HIP_TRY(lbn.alloc(nbnd * sizeof(int)));
+        HIP_TRY(cnt.alloc((size_t)(nb + 1) * sizeof(int)));
+        HIP_TRY(hipMemsetAsync(cnt.as<int>() + nb, 0, sizeof(int), st));
+        size_t tb = 0;
+        HIP_TRY(tcsc::plan_scan_tmp_bytes(nb + 1, &tb));
+        HIP_TRY(tmp.alloc(tb));
+        po.lbp = lbp.as<int>();
+        po.lbn = lbn.as<int>();
+        po.cnt = cnt.as<int>();
+        po.scan_tmp = tmp.p;
+        po.scan_tmp_bytes = tb;
+        HIP_TRY(tcsc::plan_build(in, po, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    *out = plan.release();
+    return TCSC_OK;
+}
+
+class DeviceGuard {
+  public:
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+        ok_ = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev_ >= 0) (void)hipSetDevice(prev_);
+    }
+    bool ok() const { return ok_; }
+
+  private:
+    int prev_ = -1;
+    bool ok_ = false;
+};
+
+}  // namespace
+
+// ===========================================================================
+// Device-pointer API (include/tcsc_gpu.h)
+// ===========================================================================
+extern "C" {
+
+int tcsc_gpu_device_count(void) { return device_count_raw(); }
+
+const char* tcsc_gpu_last_error(void) { return g_last_error.c_str(); }
+
+int tcsc_gpu_plan_create(const tcsc_t* W, int col_begin, int col_end, int device, void* stream,
+                         tcsc_gpu_plan** out) {
+    if (!W || !out || col_begin < 0 || col_end > W->cols || col_begin > col_end || W->rows < 0) {
+        set_error("tcsc_gpu_plan_create: bad arguments");
+        return TCSC_E_ARG;
+    }
+    *out = nullptr;
+    const int nc = col_end - col_begin;
+    DeviceGuard dg(device);
+    if (!dg.ok()) {
+        set_error("tcsc_gpu_plan_create: cannot select device %d", device);
+        return TCSC_E_NODEV;
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int p0 = W->col_start_pos[col_begin], p1 = W->col_start_pos[col_end];
+    const int q0 = W->col_start_neg[col_begin], q1 = W->col_start_neg[col_end];
+    // column slice, rebased to 0
+    std::vector<int> csp(nc + 1), csn(nc + 1);
+    for (int j = 0; j <= nc; ++j) {
+        csp[j] = W->col_start_pos[col_begin + j] - p0;
+        csn[j] = W->col_start_neg[col_begin + j] - q0;
+    }
+    DevBuf dcsp, dcsn, drip, drin;
+    HIP_TRY(dcsp.alloc((nc + 1) * sizeof(int)));
+    HIP_TRY(dcsn.alloc((nc + 1) * sizeof(int)));
+    HIP_TRY(drip.alloc((size_t)(p1 - p0) * sizeof(int)));
+    HIP_TRY(drin.alloc((size_t)(q1 - q0) * sizeof(int)));
+    HIP_TRY(hipMemcpyAsync(dcsp.p, csp.data(), (nc + 1) * sizeof(int), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(dcsn.p, csn.data(), (nc + 1) * sizeof(int), hipMemcpyHostToDevice, st));
+    if (p1 > p0)
+        HIP_TRY(hipMemcpyAsync(drip.p, W->row_index_pos + p0, (size_t)(p1 - p0) * sizeof(int),
+                               hipMemcpyHostToDevice, st));
+    if (q1 > q0)
+        HIP_TRY(hipMemcpyAsync(drin.p, W->row_index_neg + q0, (size_t)(q1 - q0) * sizeof(int),
+                               hipMemcpyHostToDevice, st));
+    int rc = build_plan(W->rows, 0, nc, p1 - p0, q1 - q0, dcsp.as<int>(), dcsn.as<int>(), drip.as<int>(),
+                        drin.as<int>(), device, st, out);
+    if (rc == TCSC_OK) (*out)->col_begin = col_begin;
+    return rc;
+}
+
+int tcsc_gpu_plan_create_device(int rows, int cols, const int* d_csp, const int* d_csn, const int* d_rip,
+                                const int* d_rin, int col_begin, int col_end, int device, void* stream,
+                                tcsc_gpu_plan** out) {
+    if (!out || !d_csp || !d_csn || col_begin < 0 || col_end > cols || col_begin > col_end || rows < 0) {
+        set_error("tcsc_gpu_plan_create_device: bad arguments");
+        return TCSC_E_ARG;
+    }
+    *out = nullptr;
+    DeviceGuard dg(device);
+    if (!dg.ok()) {
+        set_error("tcsc_gpu_plan_create_device: cannot select device %d", device);
+        return TCSC_E_NODEV;
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int ends[4];
+    HIP_TRY(hipMemcpyAsync(&ends[0], d_csp + col_begin, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&ends[1], d_csp + col_end, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&ends[2], d_csn + col_begin, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&ends[3], d_csn + col_end, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return build_plan(rows, col_begin, col_end - col_begin, ends[1] - ends[0], ends[3] - ends[2], d_csp, d_csn,
+                      d_rip, d_rin, device, st, out);
+}
+
+int tcsc_gpu_plan_get_info(const tcsc_gpu_plan* p, tcsc_gpu_plan_info* info) {
+    if (!p || !info) {
+        set_error("tcsc_gpu_plan_get_info: NULL");
+        return TCSC_E_ARG;
+    }
+    info->device = p->device;
+    info->rows = p->rows;
+    info->cols = p->cols;
+    info->col_begin = p->col_begin;
+    info->nnz = p->n_pos + p->n_neg;
+    info->n_pos = p->n_pos;
+    info->n_neg = p->n_neg;
+    info->chunk_k = p->chunk_k;
+    info->n_chunks = p->n_chunks;
+    info->device_bytes = p->bytes;
+    return TCSC_OK;
+}
+
+void tcsc_gpu_plan_destroy(tcsc_gpu_plan* p) {
+    if (!p) return;
+    DeviceGuard dg(p->device);
+    if (p->ent) (void)hipFree(p->ent);
+    if (p->cptr) (void)hipFree(p->cptr);
+    delete p;
+}
+
+int tcsc_gpu_sgemm(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy,
+                   int variant, float a, void* stream) {
+    if (!p || M < 0 || ldy < p->cols || variant < 0 || variant > 4) {
+        set_error("tcsc_gpu_sgemm: bad arguments (M=%d ldy=%d variant=%d)", M, ldy, variant);
+        return TCSC_E_ARG;
+    }
+    if (M == 0 || p->cols == 0) return TCSC_OK;
+    if (!dY || !dB || (!dX && p->rows > 0)) {
+        set_error("tcsc_gpu_sgemm: NULL device pointer");
+        return TCSC_E_ARG;
+    }
+    tcsc::GemmArgs g;
+    g.X = dX;
+    g.M = M;
+    g.K = p->rows;
+    g.ent = p->ent;
+    g.cptr = p->cptr;
+    g.ncols = p->cols;
+    g.chunk_k = p->chunk_k;
+    g.B = dB;
+    g.Y = dY;
+    g.ldy = ldy;
+    g.a = a;
+    // Bias first for tcsc_sgemm_basic (tcsc.c:74-96), last otherwise
+    // (tcsc.c:149-161; the optimized family adds per-sign partial sums to
+    // the bias, which no single accumulation order reproduces: DESIGN.md).
+    g.bias_first = (variant == TCSC_VARIANT_BASIC);
+    g.prelu = (variant >= TCSC_VARIANT_PRELU_BASIC);
+    hipError_t e = tcsc::launch_gemm(g, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "tcsc_gpu_sgemm launch");
+    return TCSC_OK;
+}
+
+int tcsc_gpu_from_dense(const float* d_dense, int rows, int cols, int* d_csp, int* d_csn, int* d_rip, int* d_rin,
+                        int* n_pos, int* n_neg, void* stream) {
+    if (!d_csp || !d_csn || !n_pos || !n_neg || rows < 0 || cols < 0 || (!d_dense && rows * (long long)cols)) {
+        set_error("tcsc_gpu_from_dense: bad arguments");
+        return TCSC_E_ARG;
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    DevBuf cntp, cntn, tmp;
+    HIP_TRY(cntp.alloc((size_t)(cols + 1) * sizeof(int)));
+    HIP_TRY(cntn.alloc((size_t)(cols + 1) * sizeof(int)));
+    HIP_TRY(hipMemsetAsync(cntp.p, 0, (size_t)(cols + 1) * sizeof(int), st));
+    HIP_TRY(hipMemsetAsync(cntn.p, 0, (size_t)(cols + 1) * sizeof(int), st));
+    if (cols > 0 && rows > 0)
+        HIP_TRY(tcsc::dense_to_tcsc_counts(d_dense, rows, cols, cntp.as<int>(), cntn.as<int>(), st));
+    size_t tb = 0;
+    HIP_TRY(tcsc::plan_scan_tmp_bytes(cols + 1, &tb));
+    HIP_TRY(tmp.alloc(tb));
+    HIP_TRY(tcsc::exclusive_scan_i32(cntp.as<int>(), d_csp, cols + 1, tmp.p, tb, st));
+    HIP_TRY(tcsc::exclusive_scan_i32(cntn.as<int>(), d_csn, cols + 1, tmp.p, tb, st));
+    int tot[2];
+    HIP_TRY(hipMemcpyAsync(&tot[0], d_csp + cols, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&tot[1], d_csn + cols, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    *n_pos = tot[0];
+    *n_neg = tot[1];
+    if (d_rip && d_rin && cols > 0 && rows > 0) {
+        HIP_TRY(tcsc::dense_to_tcsc_fill(d_dense, rows, cols, d_csp, d_csn, d_rip, d_rin, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return TCSC_OK;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// Host-pointer API (include/sparse/tcsc.h)
+// ===========================================================================
+namespace {
+
+// One column block of W on one device.
+struct Shard {
+    int device = 0;
+    int c0 = 0, c1 = 0;
+    tcsc_gpu_plan* plan = nullptr;
+};
+
+struct CacheEntry {
+    // fingerprint: a tcsc_t is immutable after construction in the
+    // reference (SURVEY.md §8b "Ownership"); the fingerprint still guards
+    // against a caller rebuilding the arrays in place.
+    int rows = 0, cols = 0, n_pos = 0, n_neg = 0;
+    const int *csp = nullptr, *csn = nullptr, *rip = nullptr, *rin = nullptr;
+    std::vector<Shard> shards;
+};
+
+// Per-device staging buffers for X, B and Y of the host API.
+struct DevState {
+    hipStream_t stream = nullptr;
+    float *x = nullptr, *b = nullptr, *y = nullptr;
+    size_t x_cap = 0, b_cap = 0, y_cap = 0;
+};
+
+std::mutex g_mu;  // guards everything below (host API is re-entrant, not concurrent-fast)
+std::unordered_map<const tcsc_t*, CacheEntry> g_cache;
+std::vector<DevState> g_dev;
+int g_shards_override = 0;
+
+void destroy_entry(CacheEntry& e) {
+    for (auto& s : e.shards) tcsc_gpu_plan_destroy(s.plan);
+    e.shards.clear();
+}
+
+bool fingerprint_matches(const CacheEntry& e, const tcsc_t* W) {
+    return e.rows == W->rows && e.cols == W->cols && e.n_pos == W->n_elem_pos && e.n_neg == W->n_elem_neg &&
+           e.csp == W->col_start_pos && e.csn == W->col_start_neg && e.rip == W->row_index_pos &&
+           e.rin == W->row_index_neg;
+}
+
+[[noreturn]] void die() {
+    std::fprintf(stderr, "[tcsc_amd] fatal: %s\n", g_last_error.c_str());
+    std::abort();
+}
+
+void report(int rc) {
+    if (rc == TCSC_OK) return;
+    const char* pol = std::getenv("TCSC_ON_ERROR");
+    if (pol && std::strcmp(pol, "continue") == 0) {
+        std::fprintf(stderr, "[tcsc_amd] error: %s\n", g_last_error.c_str());
+        return;
+    }
+    die();
+}
+
+int ensure(float** p, size_t* cap, size_t bytes) {
+    if (*cap >= bytes && *p) return TCSC_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    size_t want = bytes < 256 ? 256 : bytes;
+    HIP_TRY(hipMalloc(p, want));
+    *cap = want;
+    return TCSC_OK;
+}
+
+int num_shards_locked(int ndev) {
+    if (g_shards_override > 0) return g_shards_override;
+    int n = ndev;
+    if (const char* s = std::getenv("TCSC_NUM_GPUS")) {
+        int v = std::atoi(s);
+        if (v > 0 && v < n) n = v;
+    }
+    return n < 1 ? 1 : n;
+}
+
+int get_entry_locked(const tcsc_t* W, CacheEntry** out) {
+    const int ndev = device_count_raw();
+    if (ndev <= 0) {
+        set_error("no HIP device visible: the TCSC kernels need a gfx950 GPU");
+        return TCSC_E_NODEV;
+    }
+    if ((int)g_dev.size() < ndev) g_dev.resize(ndev);
+    auto it = g_cache.find(W);
+    if (it != g_cache.end()) {
+        if (fingerprint_matches(it->second, W)) {
+            *out = &it->second;
+            return TCSC_OK;
+        }
+        destroy_entry(it->second);
+        g_cache.erase(it);
+    }
+    CacheEntry e;
+    e.rows = W->rows;
+    e.cols = W->cols;
+    e.n_pos = W->n_elem_pos;
+    e.n_neg = W->n_elem_neg;
+    e.csp = W->col_start_pos;
+    e.csn = W->col_start_neg;
+    e.rip = W->row_index_pos;
+    e.rin = W->row_index_neg;
+    int S = num_shards_locked(ndev);
+    if (S > W->cols && W->cols > 0) S = W->cols;
+    if (S < 1) S = 1;
+    for (int s = 0; s < S; ++s) {
+        Shard sh;
+        sh.device = s % ndev;
+        sh.c0 = (int)((long long)W->cols * s / S);
+        sh.c1 = (int)((long long)W->cols * (s + 1) / S);
+        DevState& ds = g_dev[sh.device];
+        {
+            DeviceGuard dg(sh.device);
+            if (!ds.stream) HIP_TRY(hipStreamCreateWithFlags(&ds.stream, hipStreamNonBlocking));
+        }
+        int rc = tcsc_gpu_plan_create(W, sh.c0, sh.c1, sh.device, ds.stream, &sh.plan);
+        if (rc != TCSC_OK) {
+            destroy_entry(e);
+            return rc;
+        }
+        e.shards.push_back(sh);
+    }
+    auto res = g_cache.emplace(W, std::move(e));
+    *out = &res.first->second;
+    return TCSC_OK;
+}
+
+// Everything one device does for one call: H2D X once, then per shard:
+// H2D bias slice, launch, D2H of the M x (c1-c0) block into Y's columns.
+int run_device(int dev, const std::vector<const Shard*>& shards, const float* X, const float* B, float* Y,
+               int M, int N, int K, int variant, float a) {
+    DeviceGuard dg(dev);
+    DevState& ds = g_dev[dev];
+    hipStream_t st = ds.stream;
+    const size_t xb = (size_t)M * K * sizeof(float);
+    int rc;
+    if ((rc = ensure(&ds.x, &ds.x_cap, xb)) != TCSC_OK) return rc;
+    if (xb) HIP_TRY(hipMemcpyAsync(ds.x, X, xb, hipMemcpyHostToDevice, st));
+    for (const Shard* sh : shards) {
+        const int nc = sh->c1 - sh->c0;
+        if (nc == 0) continue;
+        if ((rc = ensure(&ds.b, &ds.b_cap, (size_t)nc * sizeof(float))) != TCSC_OK) return rc;
+        if ((rc = ensure(&ds.y, &ds.y_cap, (size_t)M * nc * sizeof(float))) != TCSC_OK) return rc;
+        HIP_TRY(hipMemcpyAsync(ds.b, B + sh->c0, (size_t)nc * sizeof(float), hipMemcpyHostToDevice, st));
+        if ((rc = tcsc_gpu_sgemm(sh->plan, ds.x, ds.b, ds.y, M, nc, variant, a, st)) != TCSC_OK) return rc;
+        HIP_TRY(hipMemcpy2DAsync(Y + sh->c0, (size_t)N * sizeof(float), ds.y, (size_t)nc * sizeof(float),
+                                 (size_t)nc * sizeof(float), M, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    return TCSC_OK;
+}
+
+void host_sgemm(int variant, const float* X, const tcsc_t* W, const float* B, float a, float* Y, int M, int N,
+                int K) {
+    if (M <= 0 || N <= 0) return;
+    if (!W || W->cols != N || W->rows != K || !Y || !B || (!X && K > 0)) {
+        set_error("tcsc_sgemm: shape mismatch (W %dx%d, M=%d N=%d K=%d) or NULL", W ? W->rows : -1,
+                  W ? W->cols : -1, M, N, K);
+        report(TCSC_E_ARG);
+        return;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    CacheEntry* e = nullptr;
+    int rc = get_entry_locked(W, &e);
+    if (rc != TCSC_OK) {
+        report(rc);
+        return;
+    }
+    // group shards by device
+    std::vector<std::vector<const Shard*>> per_dev(g_dev.size());
+    for (const auto& s : e->shards) per_dev[s.device].push_back(&s);
+    std::vector<int> used;
+    for (size_t d = 0; d < per_dev.size(); ++d)
+        if (!per_dev[d].empty()) used.push_back((int)d);
+    if (used.size() == 1) {
+        rc = run_device(used[0], per_dev[used[0]], X, B, Y, M, N, K, variant, a);
+    } else {
+        std::vector<int> rcs(used.size(), TCSC_OK);
+        std::vector<std::string> errs(used.size());
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < used.size(); ++i)
+            th.emplace_back([&, i] {
+                rcs[i] = run_device(used[i], per_dev[used[i]], X, B, Y, M, N, K, variant, a);
+                if (rcs[i] != TCSC_OK) errs[i] = g_last_error;  // thread-local
+            });
+        for (auto& t : th) t.join();
+        for (size_t i = 0; i < used.size(); ++i)
+            if (rcs[i] != TCSC_OK) {
+                g_last_error = errs[i];
+                rc = rcs[i];
+                break;
+            }
+    }
+    report(rc);
+}
+
+}  // namespace
+
+extern "C" {
+
+void tcsc_gpu_cache_clear(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto& kv : g_cache) destroy_entry(kv.second);
+    g_cache.clear();
+}
+
+int tcsc_gpu_num_shards(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return num_shards_locked(device_count_raw());
+}
+
+void tcsc_gpu_set_num_shards(int shards) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_shards_override = shards > 0 ? shards : 0;
+    for (auto& kv : g_cache) destroy_entry(kv.second);
+    g_cache.clear();
+}
+
+void tcsc_sgemm_basic(const dense_t X, const tcsc_t* W, const dense_t B, dense_t Y, int M, int N, int K) {
+    host_sgemm(TCSC_VARIANT_BASIC, X, W, B, 0.0f, Y, M, N, K);
+}
+
+void tcsc_sgemm_optimized(const dense_t X, const tcsc_t* W, const dense_t B, dense_t Y, int M, int N, int K) {
+    host_sgemm(TCSC_VARIANT_OPTIMIZED, X, W, B, 0.0f, Y, M, N, K);
+}
+
+void tcsc_sgemm_prelu_basic(const dense_t X, const tcsc_t* W, const dense_t B, float a, dense_t Y, int M, int N,
+                            int K) {
+    host_sgemm(TCSC_VARIANT_PRELU_BASIC, X, W, B, a, Y, M, N, K);
+}
+
+void tcsc_sgemm_prelu_optimized_separate(const dense_t X, const tcsc_t* W, const dense_t B, float a, dense_t Y,
+                                         int M, int N, int K) {
+    host_sgemm(TCSC_VARIANT_PRELU_SEPARATE, X, W, B, a, Y, M, N, K);
+}
+
+void tcsc_sgemm_prelu_optimized_onthego(const dense_t X, const tcsc_t* W, const dense_t B, float a, dense_t Y,
+                                        int M, int N, int K) {
+    host_sgemm(TCSC_VARIANT_PRELU_ONTHEGO, X, W, B, a, Y, M, N, K);
+}
+
+void tcsc_free(tcsc_t* W) {
+    if (!W) return;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_cache.find(W);
+        if (it != g_cache.end()) {
+            destroy_entry(it->second);
+            g_cache.erase(it);
+        }
+    }
+    std::free(W->col_start_pos);
+    std::free(W->col_start_neg);
+    std::free(W->row_index_pos);
+    std::free(W->row_index_neg);
+    std::free(W);
+}
+
+}  // extern "C"

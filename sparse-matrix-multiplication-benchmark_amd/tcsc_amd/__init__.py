@@ -1,0 +1,278 @@
+"""Python mirror of the TCSC drop-in API (ctypes over libtcsc_amd.so).
+
+Names and argument order follow the reference's C API (sparse/tcsc.h:19-48,
+argument order (M, N, K) handled internally); numpy arrays stand in for
+``dense_t`` and :class:`TcscMatrix` owns a ``tcsc_t*`` created by the
+library's ``tcsc_from_dense``.  The device API of include/tcsc_gpu.h is
+exposed through :class:`Plan`, which takes raw device pointers (ints) or
+torch tensors.
+
+There is no CPU fallback: importing works without a GPU (so the ABI can be
+checked on a build host), but every compute call needs the gfx950 HIP
+library and a visible device, and raises :class:`TcscError` otherwise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libtcsc_amd.so")
+
+VARIANTS = ("basic", "optimized", "prelu_basic", "prelu_separate", "prelu_onthego")
+VARIANT_ID = {v: i for i, v in enumerate(VARIANTS)}
+PRELU_VARIANTS = frozenset(VARIANTS[2:])
+
+# every symbol include/*.h declares (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = (
+    # include/sparse/tcsc.h
+    "tcsc_from_dense", "tcsc_sgemm_basic", "tcsc_sgemm_optimized", "tcsc_sgemm_prelu_basic",
+    "tcsc_sgemm_prelu_optimized_separate", "tcsc_sgemm_prelu_optimized_onthego", "tcsc_free",
+    # include/dense/dense.h
+    "dense_random", "init_rand_dense", "init_rand_sparse", "compare", "gemm_basic", "gemm_prelu_basic",
+    "tcsc_set_seed",
+    # include/tcsc_gpu.h
+    "tcsc_gpu_device_count", "tcsc_gpu_plan_create", "tcsc_gpu_plan_create_device", "tcsc_gpu_plan_get_info",
+    "tcsc_gpu_plan_destroy", "tcsc_gpu_sgemm", "tcsc_gpu_from_dense", "tcsc_gpu_last_error",
+    "tcsc_gpu_cache_clear", "tcsc_gpu_num_shards", "tcsc_gpu_set_num_shards",
+)
+
+
+class TcscError(RuntimeError):
+    pass
+
+
+class tcsc_t(C.Structure):
+    """Layout of tcsc_t (include/sparse/tcsc.h; reference sparse/tcsc.h:6-17)."""
+
+    _fields_ = [
+        ("rows", C.c_int), ("cols", C.c_int), ("n_elem_pos", C.c_int), ("n_elem_neg", C.c_int),
+        ("col_start_pos", C.POINTER(C.c_int)), ("col_start_neg", C.POINTER(C.c_int)),
+        ("row_index_pos", C.POINTER(C.c_int)), ("row_index_neg", C.POINTER(C.c_int)),
+    ]
+
+
+class plan_info_t(C.Structure):
+    _fields_ = [
+        ("device", C.c_int), ("rows", C.c_int), ("cols", C.c_int), ("col_begin", C.c_int),
+        ("nnz", C.c_longlong), ("n_pos", C.c_longlong), ("n_neg", C.c_longlong),
+        ("chunk_k", C.c_int), ("n_chunks", C.c_int), ("device_bytes", C.c_size_t),
+    ]
+
+
+_f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile lib/libtcsc_amd.so (hipcc --offload-arch=gfx950)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", PKG_DIR, "-j8"])
+    return LIB_PATH
+
+
+def lib():
+    """Load the library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise TcscError(f"{LIB_PATH} missing: build it with `make -C {PKG_DIR}`")
+    L = C.CDLL(LIB_PATH)
+    vp, i, f = C.c_void_p, C.c_int, C.c_float
+    P = C.POINTER(tcsc_t)
+    L.tcsc_from_dense.argtypes = [_f32p, i, i]
+    L.tcsc_from_dense.restype = P
+    for n in ("tcsc_sgemm_basic", "tcsc_sgemm_optimized"):
+        getattr(L, n).argtypes = [_f32p, P, _f32p, _f32p, i, i, i]
+        getattr(L, n).restype = None
+    for n in ("tcsc_sgemm_prelu_basic", "tcsc_sgemm_prelu_optimized_separate",
+              "tcsc_sgemm_prelu_optimized_onthego"):
+        getattr(L, n).argtypes = [_f32p, P, _f32p, f, _f32p, i, i, i]
+        getattr(L, n).restype = None
+    L.tcsc_free.argtypes = [P]
+    L.tcsc_free.restype = None
+    L.tcsc_set_seed.argtypes = [C.c_ulonglong]
+    L.tcsc_gpu_device_count.restype = i
+    L.tcsc_gpu_last_error.restype = C.c_char_p
+    L.tcsc_gpu_plan_create.argtypes = [P, i, i, i, vp, C.POINTER(vp)]
+    L.tcsc_gpu_plan_create_device.argtypes = [i, i, vp, vp, vp, vp, i, i, i, vp, C.POINTER(vp)]
+    L.tcsc_gpu_plan_get_info.argtypes = [vp, C.POINTER(plan_info_t)]
+    L.tcsc_gpu_plan_destroy.argtypes = [vp]
+    L.tcsc_gpu_plan_destroy.restype = None
+    L.tcsc_gpu_sgemm.argtypes = [vp, vp, vp, vp, i, i, i, f, vp]
+    L.tcsc_gpu_from_dense.argtypes = [vp, i, i, vp, vp, vp, vp, C.POINTER(i), C.POINTER(i), vp]
+    L.tcsc_gpu_num_shards.restype = i
+    L.tcsc_gpu_set_num_shards.argtypes = [i]
+    L.tcsc_gpu_set_num_shards.restype = None
+    L.tcsc_gpu_cache_clear.restype = None
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    return lib().tcsc_gpu_last_error().decode(errors="replace")
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise TcscError(f"{what} failed (status {rc}): {last_error()}")
+
+
+def device_count() -> int:
+    return int(lib().tcsc_gpu_device_count())
+
+
+def require_gpu() -> None:
+    if device_count() <= 0:
+        raise TcscError("no HIP device visible: the TCSC kernels need a gfx950 (MI355X) GPU")
+
+
+class TcscMatrix:
+    """Owns a ``tcsc_t*`` (tcsc_from_dense / tcsc_free, sparse/tcsc.h:19,48)."""
+
+    def __init__(self, ptr):
+        if not ptr:
+            raise TcscError("tcsc_from_dense returned NULL")
+        self.ptr = ptr
+
+    @classmethod
+    def from_dense(cls, dense: np.ndarray) -> "TcscMatrix":
+        dense = np.ascontiguousarray(dense, dtype=np.float32)
+        rows, cols = dense.shape
+        buf = dense.reshape(-1) if dense.size else np.zeros(1, np.float32)
+        return cls(lib().tcsc_from_dense(buf, rows, cols))
+
+    @property
+    def rows(self) -> int:
+        return self.ptr.contents.rows
+
+    @property
+    def cols(self) -> int:
+        return self.ptr.contents.cols
+
+    @property
+    def nnz(self) -> int:
+        t = self.ptr.contents
+        return t.n_elem_pos + t.n_elem_neg
+
+    def arrays(self):
+        """(col_start_pos, col_start_neg, row_index_pos, row_index_neg) copies."""
+        t = self.ptr.contents
+
+        def take(p, n):
+            return np.ctypeslib.as_array(p, shape=(n,)).copy() if n > 0 else np.zeros(0, np.int32)
+
+        return (take(t.col_start_pos, t.cols + 1), take(t.col_start_neg, t.cols + 1),
+                take(t.row_index_pos, t.n_elem_pos), take(t.row_index_neg, t.n_elem_neg))
+
+    def free(self) -> None:
+        if self.ptr:
+            lib().tcsc_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def sgemm(variant: str, X: np.ndarray, W: TcscMatrix, B: np.ndarray, a: float = 0.2,
+          Y: np.ndarray | None = None) -> np.ndarray:
+    """Host-pointer call of tcsc_sgemm_<variant> (sparse/tcsc.h:21-46)."""
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    M, K = X.shape
+    N = W.cols
+    B = np.ascontiguousarray(B, dtype=np.float32).reshape(-1)
+    if Y is None:
+        Y = np.empty((M, N), np.float32)
+    L = lib()
+    nz = lambda a_: a_.reshape(-1) if a_.size else np.zeros(1, np.float32)  # noqa: E731
+    if variant in PRELU_VARIANTS:
+        name = "tcsc_sgemm_prelu_basic" if variant == "prelu_basic" else "tcsc_sgemm_" + variant.replace(
+            "prelu_", "prelu_optimized_")
+        getattr(L, name)(nz(X), W.ptr, nz(B), a, nz(Y), M, N, K)
+    else:
+        getattr(L, "tcsc_sgemm_" + variant)(nz(X), W.ptr, nz(B), nz(Y), M, N, K)
+    return Y
+
+
+def set_num_shards(n: int) -> None:
+    lib().tcsc_gpu_set_num_shards(int(n))
+
+
+def num_shards() -> int:
+    return int(lib().tcsc_gpu_num_shards())
+
+
+def cache_clear() -> None:
+    lib().tcsc_gpu_cache_clear()
+
+
+def _ptr(x) -> int:
+    if x is None:
+        return 0
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):  # torch tensor
+        return int(x.data_ptr())
+    raise TypeError(f"expected a device pointer or tensor, got {type(x)}")
+
+
+class Plan:
+    """Device plan for columns [col_begin, col_end) of W (include/tcsc_gpu.h)."""
+
+    def __init__(self, W: TcscMatrix, col_begin: int = 0, col_end: int | None = None, device: int = 0,
+                 stream: int = 0):
+        col_end = W.cols if col_end is None else col_end
+        h = C.c_void_p()
+        _check(lib().tcsc_gpu_plan_create(W.ptr, col_begin, col_end, device, C.c_void_p(stream), C.byref(h)),
+               "tcsc_gpu_plan_create")
+        self.handle = h
+
+    @classmethod
+    def from_device(cls, rows, cols, csp, csn, rip, rin, col_begin=0, col_end=None, device=0, stream=0):
+        self = cls.__new__(cls)
+        col_end = cols if col_end is None else col_end
+        h = C.c_void_p()
+        _check(lib().tcsc_gpu_plan_create_device(rows, cols, C.c_void_p(_ptr(csp)), C.c_void_p(_ptr(csn)),
+                                                 C.c_void_p(_ptr(rip)), C.c_void_p(_ptr(rin)), col_begin,
+                                                 col_end, device, C.c_void_p(stream), C.byref(h)),
+               "tcsc_gpu_plan_create_device")
+        self.handle = h
+        return self
+
+    def info(self) -> dict:
+        inf = plan_info_t()
+        _check(lib().tcsc_gpu_plan_get_info(self.handle, C.byref(inf)), "tcsc_gpu_plan_get_info")
+        return {k: getattr(inf, k) for k, _ in plan_info_t._fields_}
+
+    def sgemm(self, X, B, Y, M: int, ldy: int, variant: str = "prelu_basic", a: float = 0.2,
+              stream: int = 0) -> None:
+        _check(lib().tcsc_gpu_sgemm(self.handle, C.c_void_p(_ptr(X)), C.c_void_p(_ptr(B)), C.c_void_p(_ptr(Y)),
+                                    int(M), int(ldy), VARIANT_ID[variant], float(a), C.c_void_p(stream)),
+               "tcsc_gpu_sgemm")
+
+    def destroy(self) -> None:
+        if getattr(self, "handle", None):
+            lib().tcsc_gpu_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def gpu_from_dense(d_dense, rows: int, cols: int, d_csp, d_csn, d_rip=None, d_rin=None, stream: int = 0):
+    """Device tcsc_from_dense; returns (n_pos, n_neg)."""
+    p, q = C.c_int(), C.c_int()
+    _check(lib().tcsc_gpu_from_dense(C.c_void_p(_ptr(d_dense)), rows, cols, C.c_void_p(_ptr(d_csp)),
+                                     C.c_void_p(_ptr(d_csn)), C.c_void_p(_ptr(d_rip)), C.c_void_p(_ptr(d_rin)),
+                                     C.byref(p), C.byref(q), C.c_void_p(stream)), "tcsc_gpu_from_dense")
+    return p.value, q.value

@@ -1,0 +1,124 @@
+"""The drop-in boundary, checked without a GPU: the C-ABI library loads and
+exports every symbol include/*.h declares, the headers are valid C and C++,
+and the host-side format builder is bit-exact with the reference."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_NAMES, PKG, ROOT, load_golden, tcsc_of
+
+import tcsc_amd
+
+
+@pytest.fixture(scope="module")
+def built_lib():
+    tcsc_amd.build()
+    return tcsc_amd.lib()
+
+
+def declared_functions():
+    names = set()
+    for h in ("include/sparse/tcsc.h", "include/dense/dense.h", "include/tcsc_gpu.h"):
+        src = open(os.path.join(ROOT, h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"//[^\n]*", "", src)
+        for m in re.finditer(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", src):
+            name = m.group(1)
+            if name not in ("if", "sizeof", "defined") and not name.isupper():
+                names.add(name)
+    return names
+
+
+def test_every_declared_symbol_is_exported(built_lib):
+    declared = declared_functions()
+    assert declared == set(tcsc_amd.EXPORTED_SYMBOLS), declared ^ set(tcsc_amd.EXPORTED_SYMBOLS)
+    out = subprocess.check_output(["nm", "-D", "--defined-only", tcsc_amd.LIB_PATH], text=True)
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = declared - exported
+    assert not missing, missing
+    for name in declared:
+        assert hasattr(built_lib, name)
+
+
+def test_reference_signatures_have_c_linkage():
+    """main.cpp's function-pointer types (main.cpp:54,116) bind to these
+    unmangled symbols when recompiled against include/."""
+    out = subprocess.check_output(["nm", "-D", "--defined-only", tcsc_amd.LIB_PATH], text=True)
+    for s in ("tcsc_sgemm_basic", "tcsc_sgemm_prelu_optimized_onthego", "tcsc_from_dense", "tcsc_free"):
+        assert re.search(rf"\bT {s}$", out, re.M), s
+
+
+HEADER_PROBE = r"""
+#include <sparse/tcsc.h>
+#include <tcsc_gpu.h>
+typedef void (*gemm_fn)(const dense_t, const tcsc_t *, const dense_t, dense_t, int, int, int);
+typedef void (*prelu_fn)(const dense_t, const tcsc_t *, const dense_t, float, dense_t, int, int, int);
+int main(void) {
+    gemm_fn g[2] = {tcsc_sgemm_basic, tcsc_sgemm_optimized};
+    prelu_fn p[3] = {tcsc_sgemm_prelu_basic, tcsc_sgemm_prelu_optimized_separate,
+                     tcsc_sgemm_prelu_optimized_onthego};
+    tcsc_gpu_plan_info info;
+    (void)info; (void)g; (void)p;
+    return tcsc_gpu_device_count() < 0;
+}
+"""
+
+
+@pytest.mark.parametrize("lang", ["c", "c++"])
+def test_headers_compile_and_link(tmp_path, built_lib, lang):
+    src = tmp_path / ("probe.c" if lang == "c" else "probe.cpp")
+    src.write_text(HEADER_PROBE)
+    exe = tmp_path / "probe"
+    cc = "gcc" if lang == "c" else "g++"
+    std = "-std=c99" if lang == "c" else "-std=c++17"
+    subprocess.check_call([cc, std, "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src), "-o",
+                           str(exe), "-L", os.path.dirname(tcsc_amd.LIB_PATH), "-ltcsc_amd",
+                           "-Wl,-rpath," + os.path.dirname(tcsc_amd.LIB_PATH)])
+    assert exe.exists()
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_host_tcsc_from_dense_bitexact(built_lib, name, monkeypatch):
+    monkeypatch.setenv("TCSC_BUILDER", "host")
+    g = load_golden(name)
+    W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
+    ref = tcsc_of(g)
+    got = W.arrays()
+    for a, b in zip(got, ref.arrays()):
+        np.testing.assert_array_equal(a, b)
+    assert W.rows == ref.rows and W.cols == ref.cols
+    W.free()
+
+
+def test_device_count_without_gpu_is_zero_or_more(built_lib):
+    assert tcsc_amd.device_count() >= 0
+
+
+def test_plan_create_rejects_bad_range(built_lib):
+    g = load_golden("cfg1")
+    W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
+    with pytest.raises(tcsc_amd.TcscError):
+        tcsc_amd.Plan(W, 10, 5)
+    with pytest.raises(tcsc_amd.TcscError):
+        tcsc_amd.Plan(W, 0, W.cols + 1)
+
+
+def test_gpu_entry_points_fail_loudly_without_device(built_lib):
+    if tcsc_amd.device_count() > 0:
+        pytest.skip("GPU present")
+    g = load_golden("cfg1")
+    W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
+    with pytest.raises(tcsc_amd.TcscError):
+        tcsc_amd.Plan(W)
+    # host-pointer API: no silent CPU fallback -- it reports and aborts
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, %r); import tcsc_amd;"
+        "W = tcsc_amd.TcscMatrix.from_dense(np.eye(4, dtype=np.float32));"
+        "tcsc_amd.sgemm('basic', np.ones((2,4),np.float32), W, np.zeros(4,np.float32))" % PKG
+    )
+    r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "no HIP device" in r.stderr

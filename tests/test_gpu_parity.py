@@ -1,0 +1,229 @@
+"""Parity of the gfx950 HIP path with the oracle / the reference's own
+outputs, called through the C ABI (libtcsc_amd.so).
+
+Bars:
+  * TCSC index arrays: bit-exact with tcsc_from_dense (tcsc.c:6-66).
+  * Integer-valued X: every fp32 partial sum is exact, so the outputs must
+    equal the reference's Y bit for bit, for all 5 variants.
+  * Float X: |y - y64| <= 2^-20 * (|b| + sum |x|) per element (pyoracle.TOL_REL),
+    PReLU outputs with the bound scaled by max(1, a).
+  * NaN / inf / signed-zero fixture: same classification as the reference.
+Full BASELINE sizes are checked on sampled rows against the exact fp64
+oracle, plus size-independent properties (linearity, shard concatenation).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+from conftest import GOLDEN_NAMES, load_golden, tcsc_of
+
+import tcsc_amd
+from tcsc_amd import workloads
+from tcsc_amd.shard import all_ranges
+
+pytestmark = pytest.mark.gpu
+
+EXACT_KINDS = ("int",)
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    tcsc_amd.build()
+    tcsc_amd.require_gpu()
+    tcsc_amd.set_num_shards(0)
+    return tcsc_amd.lib()
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    assert torch.cuda.is_available()
+    return torch
+
+
+def check_variant(g, variant, Y, oracle):
+    """Assert parity of a GPU output with the golden reference output."""
+    ref = g["Y_" + variant]
+    kind = g["meta"]["kind"]
+    a = float(g["a"])
+    if kind in EXACT_KINDS:
+        np.testing.assert_array_equal(Y.view(np.uint32), ref.view(np.uint32), err_msg=variant)
+        return
+    if kind == "special":
+        assert np.array_equal(np.isnan(Y), np.isnan(ref)), variant
+        assert np.array_equal(np.isinf(Y), np.isinf(ref)), variant
+        fin = np.isfinite(ref)
+        np.testing.assert_allclose(Y[fin], ref[fin], rtol=0, atol=1e-5)
+        return
+    Y64, S64 = oracle.f64_rows(g["X"], tcsc_of(g), g["B"])
+    ok, ratio = pyoracle.check_close(Y, Y64, S64, a if variant in pyoracle.PRELU_VARIANTS else None)
+    assert ok, f"{variant}: worst err/bound = {ratio:.3g}"
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_host_api_all_variants(gpu, oracle, name):
+    g = load_golden(name)
+    W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
+    for variant in pyoracle.VARIANTS:
+        Y = tcsc_amd.sgemm(variant, g["X"], W, g["B"], float(g["a"]))
+        check_variant(g, variant, Y, oracle)
+    W.free()
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_gpu_tcsc_from_dense_bitexact(gpu, name, monkeypatch):
+    monkeypatch.setenv("TCSC_BUILDER", "gpu")
+    g = load_golden(name)
+    W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
+    for a, b in zip(W.arrays(), tcsc_of(g).arrays()):
+        np.testing.assert_array_equal(a, b)
+    W.free()
+
+
+def test_device_api_matches_host_api(gpu, torch_cuda, oracle):
+    torch = torch_cuda
+    g = load_golden("cfg1")
+    W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
+    dev = torch.device("cuda:0")
+    X = torch.from_numpy(g["X"]).to(dev)
+    B = torch.from_numpy(g["B"]).to(dev)
+    M, N = g["X"].shape[0], W.cols
+    stream = torch.cuda.current_stream().cuda_stream
+    plan = tcsc_amd.Plan(W, 0, N, 0, stream)
+    for variant in pyoracle.VARIANTS:
+        Yd = torch.full((M, N + 7), 123.0, device=dev)  # ldy > N: padding untouched
+        plan.sgemm(X, B, Yd, M, N + 7, variant, float(g["a"]), stream)
+        torch.cuda.synchronize()
+        Yh = tcsc_amd.sgemm(variant, g["X"], W, g["B"], float(g["a"]))
+        out = Yd.cpu().numpy()
+        np.testing.assert_array_equal(out[:, :N], Yh)
+        assert np.all(out[:, N:] == 123.0)
+    plan.destroy()
+
+
+@pytest.mark.parametrize("shards", [2, 3, 5])
+def test_multi_shard_host_path_equals_single(gpu, shards):
+    """The column-block path (one block per GPU on a node; several blocks
+    per device here) concatenates to the single-block result bit for bit."""
+    g = load_golden("grid_m16_k512_n1024_nz8")
+    W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
+    tcsc_amd.set_num_shards(1)
+    Y1 = tcsc_amd.sgemm("prelu_onthego", g["X"], W, g["B"], 0.2)
+    tcsc_amd.set_num_shards(shards)
+    try:
+        Ys = tcsc_amd.sgemm("prelu_onthego", g["X"], W, g["B"], 0.2)
+    finally:
+        tcsc_amd.set_num_shards(0)
+    np.testing.assert_array_equal(Ys, Y1)
+
+
+def test_device_plan_from_device_arrays_and_gpu_builder(gpu, torch_cuda, oracle):
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    X = oracle.uniform((300, 777), 5)
+    Wd = oracle.ternary((777, 333), 0.05, 6)
+    B = oracle.uniform((333,), 7)
+    ref = oracle.tcsc_from_dense(Wd)
+    dWd = torch.from_numpy(Wd).to(dev)
+    csp = torch.empty(334, dtype=torch.int32, device=dev)
+    csn = torch.empty(334, dtype=torch.int32, device=dev)
+    npos, nneg = tcsc_amd.gpu_from_dense(dWd, 777, 333, csp, csn)
+    rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
+    rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
+    tcsc_amd.gpu_from_dense(dWd, 777, 333, csp, csn, rip, rin)
+    assert np.array_equal(csp.cpu().numpy(), ref.col_start_pos)
+    assert np.array_equal(rin[:nneg].cpu().numpy(), ref.row_index_neg)
+    assert np.array_equal(rip[:npos].cpu().numpy(), ref.row_index_pos)
+    # plans over sub-ranges, straight from device arrays
+    dX = torch.from_numpy(X).to(dev)
+    Y64, S64 = oracle.f64_rows(X, ref, B)
+    for c0, c1 in all_ranges(333, 4) + [(10, 11), (0, 333)]:
+        plan = tcsc_amd.Plan.from_device(777, 333, csp, csn, rip, rin, c0, c1)
+        assert plan.info()["nnz"] == int(ref.col_start_pos[c1] - ref.col_start_pos[c0]
+                                         + ref.col_start_neg[c1] - ref.col_start_neg[c0])
+        dB = torch.from_numpy(B[c0:c1].copy()).to(dev)
+        dY = torch.empty((300, c1 - c0), device=dev)
+        plan.sgemm(dX, dB, dY, 300, c1 - c0, "basic", 0.0)
+        torch.cuda.synchronize()
+        ok, ratio = pyoracle.check_close(dY.cpu().numpy(), Y64[:, c0:c1], S64[:, c0:c1])
+        assert ok, (c0, c1, ratio)
+        plan.destroy()
+
+
+def test_shape_mismatch_reports_without_writing(gpu, monkeypatch):
+    monkeypatch.setenv("TCSC_ON_ERROR", "continue")
+    g = load_golden("cfg1")
+    W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
+    X = np.ones((4, 100), np.float32)  # K != W.rows
+    Y = np.full((4, W.cols), 7.0, np.float32)
+    tcsc_amd.sgemm("basic", X, W, g["B"], 0.2, Y=Y)
+    assert np.all(Y == 7.0)
+    assert "shape mismatch" in tcsc_amd.last_error()
+
+
+def test_zero_sized_calls(gpu, torch_cuda):
+    torch = torch_cuda
+    W = tcsc_amd.TcscMatrix.from_dense(np.eye(8, dtype=np.float32))
+    Y = tcsc_amd.sgemm("basic", np.zeros((0, 8), np.float32), W, np.zeros(8, np.float32))
+    assert Y.shape == (0, 8)
+    plan = tcsc_amd.Plan(W, 3, 3)
+    plan.sgemm(torch.zeros(1, device="cuda"), torch.zeros(1, device="cuda"), torch.zeros(1, device="cuda"),
+               5, 0, "basic")
+    torch.cuda.synchronize()
+
+
+# ---------------------------------------------------------------------------
+# Full BASELINE sizes (device API, sampled-row exact checks + properties)
+# ---------------------------------------------------------------------------
+def run_device_cfg(torch, cfg, variant, x=None):
+    dev = torch.device("cuda:0")
+    inp = workloads.make_device_inputs(cfg, 0, cfg.N, dev)
+    if x is not None:
+        inp["X"] = x
+    K, N = cfg.K, cfg.N
+    csp = torch.empty(N + 1, dtype=torch.int32, device=dev)
+    csn = torch.empty(N + 1, dtype=torch.int32, device=dev)
+    npos, nneg = tcsc_amd.gpu_from_dense(inp["Wd"], K, N, csp, csn)
+    rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
+    rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
+    tcsc_amd.gpu_from_dense(inp["Wd"], K, N, csp, csn, rip, rin)
+    del inp["Wd"]
+    plan = tcsc_amd.Plan.from_device(K, N, csp, csn, rip, rin)
+    Y = torch.empty((cfg.M, N), device=dev)
+    plan.sgemm(inp["X"], inp["B"], Y, cfg.M, N, variant, 0.2)
+    torch.cuda.synchronize()
+    W = pyoracle.TCSC(K, N, csp.cpu().numpy(), csn.cpu().numpy(), rip[:npos].cpu().numpy(),
+                      rin[:nneg].cpu().numpy())
+    return inp, W, Y, plan
+
+
+@pytest.mark.parametrize("cfg_idx", [2, 3, 4, 5])
+def test_baseline_config_sampled_rows(gpu, torch_cuda, oracle, cfg_idx):
+    torch = torch_cuda
+    cfg = workloads.CONFIGS[cfg_idx]
+    inp, W, Y, plan = run_device_cfg(torch, cfg, cfg.variant)
+    rows = np.unique(np.concatenate([[0, 1, cfg.M - 1], np.random.default_rng(cfg_idx).integers(0, cfg.M, 29)]))
+    Xs = inp["X"][torch.from_numpy(rows).to(inp["X"].device)].cpu().numpy()
+    B = inp["B"].cpu().numpy()
+    Y64, S64 = oracle.f64_rows(Xs, W, B)
+    a = 0.2 if cfg.variant in pyoracle.PRELU_VARIANTS else None
+    ok, ratio = pyoracle.check_close(Y[torch.from_numpy(rows).to(Y.device)].cpu().numpy(), Y64, S64, a)
+    assert ok, f"cfg{cfg_idx}: worst err/bound {ratio:.3g}"
+    # integer-valued X at full size: exact, so bit-identical to the oracle
+    Xi = torch.randint(-512, 513, (cfg.M, cfg.K), device=inp["X"].device, dtype=torch.int32).float()
+    Yi = torch.empty_like(Y)
+    plan.sgemm(Xi, inp["B"].round(), Yi, cfg.M, cfg.N, "basic", 0.0)
+    torch.cuda.synchronize()
+    Xis = Xi[torch.from_numpy(rows).to(Xi.device)].cpu().numpy()
+    ref = oracle.sgemm("basic", Xis, W, inp["B"].round().cpu().numpy())
+    np.testing.assert_array_equal(Yi[torch.from_numpy(rows).to(Yi.device)].cpu().numpy(), ref)
+    # linearity (size-independent): Y(X1 + X2) - b == (Y(X1) - b) + (Y(X2) - b) exactly for integer X
+    Yj = torch.empty_like(Y)
+    plan.sgemm(Xi * 2, inp["B"].round(), Yj, cfg.M, cfg.N, "basic", 0.0)
+    torch.cuda.synchronize()
+    b = inp["B"].round()
+    assert torch.equal(Yj - b, 2 * (Yi - b))
+    plan.destroy()

@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprof kernel trace.
+# Stops at the first step that crashes, faults or times out (exit >= 2 that
+# is not a plain pytest failure).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+OUT=gpurun_out
+step() {  # name, timeout, cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -n 25 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+PYTEST_ARGS=${PYTEST_ARGS:-"-x -q"}
+step pytest_gpu 900 python -m pytest tests -m gpu $PYTEST_ARGS
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py ${BENCH_ARGS:-}
+if [ "${PROF:-1}" = 1 ]; then
+  export TMPDIR=/tmp
+  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-}
+fi
+echo ALL_DONE
