@@ -102,6 +102,7 @@ def main():
     tcsc_amd.gpu_from_dense(inp["Wd"], cfg.K, ncols, csp, csn, rip, rin, stream=sh)
     del inp["Wd"]
     plan = tcsc_amd.Plan.from_device(cfg.K, ncols, csp, csn, rip, rin, 0, ncols, local_rank, sh)
+    plan.reserve(cfg.M)
     nnz = npos + nneg
     X, B = inp["X"], inp["B"]
     Y = torch.empty((cfg.M, ncols), device=dev, dtype=torch.float32)
@@ -180,7 +181,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "k_tcsc_gather",
+                "kernel": "k_stream",
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_ms": kernel_s * 1e3,
                 "lds_gather_frac": (cfg.M * nnz / kernel_s) / LDS_GATHER_PEAK,

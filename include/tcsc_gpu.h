@@ -80,6 +80,12 @@ int tcsc_gpu_plan_create_device(int rows, int cols,
                                 void *stream, tcsc_gpu_plan **out);
 
 int tcsc_gpu_plan_get_info(const tcsc_gpu_plan *plan, tcsc_gpu_plan_info *info);
+
+/* Allocate the plan's split-K workspace for launches of up to `max_M` rows
+ * (small grids split K over workgroups and combine fp32 partial slabs in a
+ * fixed order).  Optional: without it tcsc_gpu_sgemm never splits.  Not
+ * thread-safe against concurrent launches of the same plan. */
+int tcsc_gpu_plan_reserve(tcsc_gpu_plan *plan, int max_M);
 void tcsc_gpu_plan_destroy(tcsc_gpu_plan *plan);
 
 /* Y[m, j] = act(B[j] + sum_{k in P(j)} X[m,k] - sum_{k in Q(j)} X[m,k])

@@ -31,9 +31,12 @@ struct tcsc_gpu_plan {
     int device = 0;
     int rows = 0, cols = 0, col_begin = 0;
     long long n_pos = 0, n_neg = 0;
-    int chunk_k = tcsc::kChunkK, n_chunks = 0;
-    int* ent = nullptr;
-    int* cptr = nullptr;
+    int n_chunks = 0, n_groups = 0;
+    long long n_entries = 0;
+    int2* ent = nullptr;   // stream entries (+ guard batch)
+    int* sptr = nullptr;   // stream starts, n_chunks*n_groups + 1
+    float* ws = nullptr;   // split-K partial slabs (tcsc_gpu_plan_reserve)
+    size_t ws_bytes = 0;
     size_t bytes = 0;
 };
 
@@ -96,56 +99,83 @@ int build_plan(int rows, int col_begin, int ncols, long long n_pos, long long n_
     plan->col_begin = col_begin;
     plan->n_pos = n_pos;
     plan->n_neg = n_neg;
-    plan->chunk_k = tcsc::kChunkK;
-    plan->n_chunks = rows > 0 ? (rows + plan->chunk_k - 1) / plan->chunk_k : 0;
-    const long long nnz = n_pos + n_neg;
-    const long long nb = (long long)plan->n_chunks * ncols;
-    if (nnz > 0x7fffffffLL - tcsc::kEntPad || nb + 1 > 0x7fffffffLL) {
-        set_error("plan too large: nnz=%lld buckets=%lld", nnz, nb);
+    plan->n_chunks = rows > 0 ? (rows + tcsc::kTK - 1) / tcsc::kTK : 0;
+    plan->n_groups = (ncols + tcsc::kCW - 1) / tcsc::kCW;
+    const int nch = plan->n_chunks, G = plan->n_groups;
+    const long long nc = (long long)nch * ncols, ng = (long long)nch * G;
+    if (n_pos + n_neg > 0x3fffffffLL || nc + 1 > 0x7fffffffLL || ng + 1 > 0x7fffffffLL) {
+        set_error("plan too large: nnz=%lld buckets=%lld", n_pos + n_neg, nc);
         return TCSC_E_ARG;
     }
-    HIP_TRY(hipMalloc(&plan->ent, (size_t)(nnz + tcsc::kEntPad) * sizeof(int)));
-    HIP_TRY(hipMalloc(&plan->cptr, (size_t)(nb + 1) * sizeof(int)));
-    plan->bytes = (size_t)(nnz + tcsc::kEntPad + nb + 1) * sizeof(int);
-    HIP_TRY(hipMemsetAsync(plan->ent, 0, (size_t)(nnz + tcsc::kEntPad) * sizeof(int), st));
-    if (nb == 0) {
-        HIP_TRY(hipMemsetAsync(plan->cptr, 0, sizeof(int), st));
-    } else {
-        tcsc::PlanDev in;
-        in.rows = rows;
-        in.ncols = ncols;
-        in.col_begin = col_begin;
-        in.n_pos = n_pos;
-        in.n_neg = n_neg;
-        in.csp = csp;
-        in.csn = csn;
-        in.rip = rip;
-        in.rin = rin;
-        tcsc::PlanOut po;
-        po.chunk_k = plan->chunk_k;
-        po.n_chunks = plan->n_chunks;
-        po.ent = plan->ent;
-        po.cptr = plan->cptr;
-        DevBuf lbp, lbn, cnt, tmp;
-        const size_t nbnd = (size_t)(plan->n_chunks + 1) * ncols;
-        HIP_TRY(lbp.alloc(nbnd * sizeof(int)));
-        HIP_TRY(lbn.alloc(nbnd * sizeof(int)));
-        HIP_TRY(cnt.alloc((size_t)(nb + 1) * sizeof(int)));
-        HIP_TRY(hipMemsetAsync(cnt.as<int>() + nb, 0, sizeof(int), st));
-        size_t tb = 0;
-        HIP_TRY(tcsc::plan_scan_tmp_bytes(nb + 1, &tb));
-        HIP_TRY(tmp.alloc(tb));
-        po.lbp = lbp.as<int>();
-        po.lbn = lbn.as<int>();
-        po.cnt = cnt.as<int>();
-        po.scan_tmp = tmp.p;
-        po.scan_tmp_bytes = tb;
-        HIP_TRY(tcsc::plan_build(in, po, st));
+    HIP_TRY(hipMalloc(&plan->sptr, (size_t)(ng + 1) * sizeof(int)));
+    if (ng == 0) {
+        HIP_TRY(hipMemsetAsync(plan->sptr, 0, sizeof(int), st));
+        HIP_TRY(hipMalloc(&plan->ent, tcsc::kBatch * sizeof(int2)));
+        HIP_TRY(hipMemsetAsync(plan->ent, 0, tcsc::kBatch * sizeof(int2), st));
         HIP_TRY(hipStreamSynchronize(st));
+        plan->bytes = sizeof(int) + tcsc::kBatch * sizeof(int2);
+        *out = plan.release();
+        return TCSC_OK;
     }
+    tcsc::PlanDev in;
+    in.rows = rows;
+    in.ncols = ncols;
+    in.col_begin = col_begin;
+    in.n_pos = n_pos;
+    in.n_neg = n_neg;
+    in.csp = csp;
+    in.csn = csn;
+    in.rip = rip;
+    in.rin = rin;
+    tcsc::PlanOut po;
+    po.n_chunks = nch;
+    po.n_groups = G;
+    po.sptr = plan->sptr;
+    DevBuf lbp, lbn, cnt, cptr, gcnt, tmp, ent;
+    const size_t nbnd = (size_t)(nch + 1) * ncols;
+    HIP_TRY(lbp.alloc(nbnd * sizeof(int)));
+    HIP_TRY(lbn.alloc(nbnd * sizeof(int)));
+    HIP_TRY(cnt.alloc((size_t)(nc + 1) * sizeof(int)));
+    HIP_TRY(cptr.alloc((size_t)(nc + 1) * sizeof(int)));
+    HIP_TRY(gcnt.alloc((size_t)(ng + 1) * sizeof(int)));
+    HIP_TRY(hipMemsetAsync(cnt.as<int>() + nc, 0, sizeof(int), st));
+    HIP_TRY(hipMemsetAsync(gcnt.as<int>() + ng, 0, sizeof(int), st));
+    size_t tb1 = 0, tb2 = 0;
+    HIP_TRY(tcsc::plan_scan_tmp_bytes(nc + 1, &tb1));
+    HIP_TRY(tcsc::plan_scan_tmp_bytes(ng + 1, &tb2));
+    HIP_TRY(tmp.alloc(tb1 > tb2 ? tb1 : tb2));
+    po.lbp = lbp.as<int>();
+    po.lbn = lbn.as<int>();
+    po.cnt = cnt.as<int>();
+    po.cptr = cptr.as<int>();
+    po.gcnt = gcnt.as<int>();
+    po.scan_tmp = tmp.p;
+    po.scan_tmp_bytes = tb1 > tb2 ? tb1 : tb2;
+    HIP_TRY(tcsc::plan_counts(in, po, st));
+    int total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, plan->sptr + ng, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    po.n_entries = total;
+    plan->n_entries = total;
+    HIP_TRY(hipMalloc(&plan->ent, (size_t)(total + tcsc::kBatch) * sizeof(int2)));
+    po.ent = plan->ent;
+    HIP_TRY(tcsc::plan_fill(in, po, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    plan->bytes = (size_t)(ng + 1) * sizeof(int) + (size_t)(total + tcsc::kBatch) * sizeof(int2);
     *out = plan.release();
     return TCSC_OK;
+}
+
+// TCSC_SLICES=n forces the split-K factor (tests, tuning); read per call.
+int slices_override() {
+    const char* s = std::getenv("TCSC_SLICES");
+    return s ? std::atoi(s) : 0;
+}
+
+size_t wanted_workspace(const tcsc_gpu_plan* p, int M) {
+    const int s = tcsc::choose_slices(M, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
+                                      slices_override());
+    return tcsc::workspace_bytes(M, p->cols, s);
 }
 
 class DeviceGuard {
@@ -164,6 +194,45 @@ class DeviceGuard {
     bool ok_ = false;
 };
 
+}  // namespace
+
+namespace {
+int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy, int variant,
+             float a, void* stream, float* ws, size_t ws_bytes) {
+    if (!p || M < 0 || ldy < p->cols || variant < 0 || variant > 4) {
+        set_error("tcsc_gpu_sgemm: bad arguments (M=%d ldy=%d variant=%d)", M, ldy, variant);
+        return TCSC_E_ARG;
+    }
+    if (M == 0 || p->cols == 0) return TCSC_OK;
+    if (!dY || !dB || (!dX && p->rows > 0)) {
+        set_error("tcsc_gpu_sgemm: NULL device pointer");
+        return TCSC_E_ARG;
+    }
+    tcsc::GemmArgs g;
+    g.X = dX;
+    g.M = M;
+    g.K = p->rows;
+    g.ent = p->ent;
+    g.sptr = p->sptr;
+    g.n_groups = p->n_groups;
+    g.ncols = p->cols;
+    g.nnz = p->n_pos + p->n_neg;
+    g.B = dB;
+    g.Y = dY;
+    g.ldy = ldy;
+    g.a = a;
+    g.ws = ws;
+    g.ws_bytes = ws ? ws_bytes : 0;
+    g.force_slices = slices_override();
+    // Bias first for tcsc_sgemm_basic (tcsc.c:74-96), last otherwise
+    // (tcsc.c:149-161; the optimized family adds per-sign partial sums to
+    // the bias, which no single accumulation order reproduces: DESIGN.md).
+    g.bias_first = (variant == TCSC_VARIANT_BASIC);
+    g.prelu = (variant >= TCSC_VARIANT_PRELU_BASIC);
+    hipError_t e = tcsc::launch_gemm(g, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "tcsc_gpu_sgemm launch");
+    return TCSC_OK;
+}
 }  // namespace
 
 // ===========================================================================
@@ -252,9 +321,9 @@ int tcsc_gpu_plan_get_info(const tcsc_gpu_plan* p, tcsc_gpu_plan_info* info) {
     info->nnz = p->n_pos + p->n_neg;
     info->n_pos = p->n_pos;
     info->n_neg = p->n_neg;
-    info->chunk_k = p->chunk_k;
+    info->chunk_k = tcsc::kTK;
     info->n_chunks = p->n_chunks;
-    info->device_bytes = p->bytes;
+    info->device_bytes = p->bytes + p->ws_bytes;
     return TCSC_OK;
 }
 
@@ -262,41 +331,31 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan* p) {
     if (!p) return;
     DeviceGuard dg(p->device);
     if (p->ent) (void)hipFree(p->ent);
-    if (p->cptr) (void)hipFree(p->cptr);
+    if (p->sptr) (void)hipFree(p->sptr);
+    if (p->ws) (void)hipFree(p->ws);
     delete p;
 }
 
+int tcsc_gpu_plan_reserve(tcsc_gpu_plan* p, int max_M) {
+    if (!p || max_M < 0) {
+        set_error("tcsc_gpu_plan_reserve: bad arguments");
+        return TCSC_E_ARG;
+    }
+    const size_t want = wanted_workspace(p, max_M);
+    if (want <= p->ws_bytes) return TCSC_OK;
+    DeviceGuard dg(p->device);
+    if (p->ws) (void)hipFree(p->ws);
+    p->ws = nullptr;
+    p->ws_bytes = 0;
+    HIP_TRY(hipMalloc(&p->ws, want));
+    p->ws_bytes = want;
+    return TCSC_OK;
+}
+
+
 int tcsc_gpu_sgemm(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy,
                    int variant, float a, void* stream) {
-    if (!p || M < 0 || ldy < p->cols || variant < 0 || variant > 4) {
-        set_error("tcsc_gpu_sgemm: bad arguments (M=%d ldy=%d variant=%d)", M, ldy, variant);
-        return TCSC_E_ARG;
-    }
-    if (M == 0 || p->cols == 0) return TCSC_OK;
-    if (!dY || !dB || (!dX && p->rows > 0)) {
-        set_error("tcsc_gpu_sgemm: NULL device pointer");
-        return TCSC_E_ARG;
-    }
-    tcsc::GemmArgs g;
-    g.X = dX;
-    g.M = M;
-    g.K = p->rows;
-    g.ent = p->ent;
-    g.cptr = p->cptr;
-    g.ncols = p->cols;
-    g.chunk_k = p->chunk_k;
-    g.B = dB;
-    g.Y = dY;
-    g.ldy = ldy;
-    g.a = a;
-    // Bias first for tcsc_sgemm_basic (tcsc.c:74-96), last otherwise
-    // (tcsc.c:149-161; the optimized family adds per-sign partial sums to
-    // the bias, which no single accumulation order reproduces: DESIGN.md).
-    g.bias_first = (variant == TCSC_VARIANT_BASIC);
-    g.prelu = (variant >= TCSC_VARIANT_PRELU_BASIC);
-    hipError_t e = tcsc::launch_gemm(g, static_cast<hipStream_t>(stream));
-    if (e != hipSuccess) return hip_fail(e, "tcsc_gpu_sgemm launch");
-    return TCSC_OK;
+    return sgemm_ws(p, dX, dB, dY, M, ldy, variant, a, stream, p ? p->ws : nullptr, p ? p->ws_bytes : 0);
 }
 
 int tcsc_gpu_from_dense(const float* d_dense, int rows, int cols, int* d_csp, int* d_csn, int* d_rip, int* d_rin,
@@ -357,8 +416,8 @@ struct CacheEntry {
 // Per-device staging buffers for X, B and Y of the host API.
 struct DevState {
     hipStream_t stream = nullptr;
-    float *x = nullptr, *b = nullptr, *y = nullptr;
-    size_t x_cap = 0, b_cap = 0, y_cap = 0;
+    float *x = nullptr, *b = nullptr, *y = nullptr, *ws = nullptr;
+    size_t x_cap = 0, b_cap = 0, y_cap = 0, ws_cap = 0;
 };
 
 std::mutex g_mu;  // guards everything below (host API is re-entrant, not concurrent-fast)
@@ -479,8 +538,11 @@ int run_device(int dev, const std::vector<const Shard*>& shards, const float* X,
         if (nc == 0) continue;
         if ((rc = ensure(&ds.b, &ds.b_cap, (size_t)nc * sizeof(float))) != TCSC_OK) return rc;
         if ((rc = ensure(&ds.y, &ds.y_cap, (size_t)M * nc * sizeof(float))) != TCSC_OK) return rc;
+        const size_t wsb = wanted_workspace(sh->plan, M);
+        if (wsb && (rc = ensure(&ds.ws, &ds.ws_cap, wsb)) != TCSC_OK) return rc;
         HIP_TRY(hipMemcpyAsync(ds.b, B + sh->c0, (size_t)nc * sizeof(float), hipMemcpyHostToDevice, st));
-        if ((rc = tcsc_gpu_sgemm(sh->plan, ds.x, ds.b, ds.y, M, nc, variant, a, st)) != TCSC_OK) return rc;
+        if ((rc = sgemm_ws(sh->plan, ds.x, ds.b, ds.y, M, nc, variant, a, st, ds.ws, ds.ws_cap)) != TCSC_OK)
+            return rc;
         HIP_TRY(hipMemcpy2DAsync(Y + sh->c0, (size_t)N * sizeof(float), ds.y, (size_t)nc * sizeof(float),
                                  (size_t)nc * sizeof(float), M, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));

@@ -6,11 +6,21 @@
 
 namespace tcsc {
 
-// K rows per LDS chunk (one 512-B LDS row per k: 128 rows x fp32).
-constexpr int kChunkK = 128;
-// Entries are padded by this many ints so unrolled scalar loads never run
-// past the allocation.
-constexpr int kEntPad = 16;
+// ---- geometry of the gather kernel (DESIGN.md "Kernel K1") ---------------
+constexpr int kTM = 256;                 // rows per workgroup: 64 lanes x 4 rows (ds_read_b128)
+constexpr int kTK = 64;                  // K rows per LDS chunk
+constexpr int kRowBytes = kTM * 4;       // one LDS row = X[m0..m0+255][k], 1 KiB
+constexpr int kBufRows = kTK + 1;        // + one row of -0.0 that padding entries point at
+constexpr int kWaves = 8;                // waves per workgroup (1 workgroup per CU)
+constexpr int kCW = 32;                  // output columns per wave (4*kCW accumulator VGPRs)
+constexpr int kBatch = 8;                // stream entries per s_load_dwordx16
+constexpr int kLdsBytes = 2 * kBufRows * kRowBytes;  // double-buffered tile: 130 KiB
+
+// Stream entry (8 bytes): word0 = +1.0f or -1.0f (bit pattern), word1 =
+// (lds_row << 10) | (4*slot); lds_row = (chunk&1)*kBufRows + (k - chunk*kTK)
+// or the pad row; slot = column inside the wave (0..kCW-1).
+static_assert(4 * kCW <= 255, "slot index must fit the 8-bit gpr_idx field");
+static_assert(64 * 16 <= 1024, "lane byte offset (16*lane) must fit the 10 low address bits");
 
 // Input TCSC arrays (device pointers, absolute offsets as in tcsc_t) and the
 // column range a plan covers.
@@ -25,15 +35,18 @@ struct PlanDev {
     const int* rin = nullptr;
 };
 
-// Plan arrays (device).  lbp/lbn/cnt/scan_tmp are build-time scratch.
+// Plan arrays (device).  Everything but ent/sptr is build-time scratch.
 struct PlanOut {
-    int chunk_k = kChunkK;
     int n_chunks = 0;
-    int* ent = nullptr;   // nnz (+kEntPad) merged entries
-    int* cptr = nullptr;  // n_chunks*ncols + 1 bucket starts (chunk-major)
+    int n_groups = 0;          // ceil(ncols / kCW) wave-column groups
+    long long n_entries = 0;   // stream entries incl. padding
+    int2* ent = nullptr;       // n_entries (+kBatch) entries
+    int* sptr = nullptr;       // n_chunks*n_groups + 1 stream starts (entries)
     int* lbp = nullptr;
     int* lbn = nullptr;
     int* cnt = nullptr;
+    int* cptr = nullptr;
+    int* gcnt = nullptr;
     void* scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
 };
@@ -41,21 +54,31 @@ struct PlanOut {
 struct GemmArgs {
     const float* X = nullptr;
     int M = 0, K = 0;
-    const int* ent = nullptr;
-    const int* cptr = nullptr;
+    const int2* ent = nullptr;
+    const int* sptr = nullptr;
+    int n_groups = 0;
     int ncols = 0;
-    int chunk_k = kChunkK;
+    long long nnz = 0;
     const float* B = nullptr;
     float* Y = nullptr;
     int ldy = 0;
     float a = 0.f;
     bool bias_first = false;
     bool prelu = false;
+    float* ws = nullptr;       // split-K partial slabs (may be null: no split)
+    size_t ws_bytes = 0;
+    int force_slices = 0;      // 0 = cost model
 };
 
-hipError_t plan_build(const PlanDev& in, PlanOut& out, hipStream_t st);
+// Plan building
 hipError_t plan_scan_tmp_bytes(long long n, size_t* bytes);
+hipError_t plan_counts(const PlanDev& in, PlanOut& out, hipStream_t st);    // -> cptr, gcnt
+hipError_t plan_fill(const PlanDev& in, PlanOut& out, hipStream_t st);      // -> sptr, ent
+// Launch
+int choose_slices(int M, int ncols, int K, long long nnz, int n_groups, size_t ws_bytes, int force);
+size_t workspace_bytes(int M, int ncols, int slices);
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st);
+// tcsc_from_dense on the device
 hipError_t dense_to_tcsc_counts(const float* D, int rows, int cols, int* cntp, int* cntn, hipStream_t st);
 hipError_t dense_to_tcsc_fill(const float* D, int rows, int cols, const int* csp, const int* csn, int* rip,
                               int* rin, hipStream_t st);

@@ -9,23 +9,27 @@
 //   tcsc_sgemm_prelu_optimized_onthego   tcsc.c:231-275
 // and tcsc_from_dense (tcsc.c:6-66) with a device builder.
 //
-// Design (DESIGN.md has the full derivation):
-//  * lanes = rows of X.  A workgroup owns TM = 128 rows (two per lane) and
-//    WAVES*CW output columns.  K is cut into chunks of TK rows; each chunk of
-//    X is staged in LDS transposed, as float2 pairs xs[k][lane] =
-//    (X[m0+2*lane][k0+k], X[m0+2*lane+1][k0+k]) -- one 512-B LDS row per k.
-//  * Every nonzero of a column is then ONE conflict-free ds_read_b64 that all
-//    64 lanes issue at the same k (the index is wave-uniform and lives in an
-//    SGPR), followed by two adds/subtracts.  No multiplies, no MFMA (W is
-//    ternary and 98 % sparse at the headline size: a dense product would do
-//    50x the work).
-//  * W is re-laid out once per tcsc_t ("plan"): the +1 and -1 lists of a
-//    column are merged in ascending k and bucketed by (chunk, column), so the
-//    entries a wave needs for one chunk are contiguous.  Entry encoding:
-//    bits 0-15 = k - k0 (row inside the chunk), bit 31 = sign (1 = -1).
-//  * Accumulators stay in VGPRs for the whole K loop; the epilogue adds the
-//    bias (first or last, matching the reference variant's order) and
-//    applies PReLU in registers before the single store of Y.
+// Kernel K1 (k_stream) -- DESIGN.md has the derivation and the measured
+// primitive rates it rests on:
+//  * lanes = rows.  A workgroup owns kTM = 256 rows of X (4 per lane) and
+//    kWaves*kCW = 256 output columns; it walks K in chunks of kTK = 64 rows.
+//    Each chunk of X is staged in LDS transposed (one 1-KiB row per k,
+//    double-buffered), so one nonzero of W is ONE conflict-free ds_read_b128
+//    that every lane issues at the same k, then two v_pk_fma_f32 with a +-1
+//    scalar (an exact add/subtract).  No multiplies of data, no MFMA: W is
+//    ternary and 98 % sparse at the headline size.
+//  * W is re-laid out once per tcsc_t (the "plan"): for every (K chunk,
+//    wave-column group) one flat stream of 8-byte entries {+-1.0f,
+//    lds_row<<10 | 4*slot}, padded to a multiple of 8.  A wave reads its
+//    stream with s_load_dwordx16 (8 entries per scalar load) and selects the
+//    accumulator of the entry's column with s_set_gpr_idx_on (relative VGPR
+//    addressing on the v_pk_fma DST/SRC2): no per-column loop, no branch per
+//    nonzero, 2 SALU + 3 VALU + 1 LDS instruction per nonzero.
+//  * Accumulators (4*kCW VGPRs) live in registers for the whole K range; the
+//    epilogue adds the bias (first or last, matching the reference variant's
+//    order) and applies PReLU before the only store of Y.  Small grids split
+//    K over workgroups (k-slices) and reduce the fp32 partial slabs in a
+//    fixed order (deterministic) in k_reduce.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
@@ -33,6 +37,8 @@
 #include "tcsc_internal.h"
 
 namespace tcsc {
+
+typedef float f32x32 __attribute__((ext_vector_type(32)));
 
 // ---------------------------------------------------------------------------
 // Plan building
@@ -46,167 +52,355 @@ __device__ __forceinline__ int lower_bound_i32(const int* __restrict__ a, int lo
     return lo;
 }
 
-// For every (chunk boundary c in [0, nch], column n): absolute position of the
-// first +1 (resp. -1) entry of column n with row >= c*TK.
+// lbp/lbn[c*ncols + n] = absolute position of the first +1 (-1) entry of
+// column n with row >= c*kTK  (c in [0, nch]; c == nch -> column end).
 __global__ void k_chunk_bounds(const int* __restrict__ csp, const int* __restrict__ csn,
                                const int* __restrict__ rip, const int* __restrict__ rin,
-                               int col_begin, int ncols, int nch, int tk, int K,
-                               int* __restrict__ lbp, int* __restrict__ lbn) {
+                               int col_begin, int ncols, int nch, int* __restrict__ lbp, int* __restrict__ lbn) {
     const long long total = (long long)(nch + 1) * ncols;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
          i += (long long)gridDim.x * blockDim.x) {
         const int c = (int)(i / ncols), n = (int)(i % ncols);
-        const int key = (c == nch) ? 0x7fffffff : c * tk;
+        const int key = (c == nch) ? 0x7fffffff : c * kTK;
         const int gn = col_begin + n;
         lbp[i] = lower_bound_i32(rip, csp[gn], csp[gn + 1], key);
         lbn[i] = lower_bound_i32(rin, csn[gn], csn[gn + 1], key);
     }
 }
 
-// cnt[c*ncols + n] = entries of column n inside chunk c.
-__global__ void k_chunk_counts(const int* __restrict__ lbp, const int* __restrict__ lbn,
-                               int ncols, int nch, int* __restrict__ cnt) {
+// cnt[c*ncols + n] = nonzeros of column n inside chunk c.
+__global__ void k_chunk_counts(const int* __restrict__ lbp, const int* __restrict__ lbn, int ncols, int nch,
+                               int* __restrict__ cnt) {
     const long long total = (long long)nch * ncols;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-         i += (long long)gridDim.x * blockDim.x) {
+         i += (long long)gridDim.x * blockDim.x)
         cnt[i] = (lbp[i + ncols] - lbp[i]) + (lbn[i + ncols] - lbn[i]);
+}
+
+// gcnt[c*G + g] = entries of group g in chunk c, rounded up to kBatch.
+__global__ void k_group_counts(const int* __restrict__ cptr, int ncols, int nch, int G, int* __restrict__ gcnt) {
+    const long long total = (long long)nch * G;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int c = (int)(i / G), g = (int)(i % G);
+        const int n0 = g * kCW, n1 = min(n0 + kCW, ncols);
+        const int real = cptr[(long long)c * ncols + n1] - cptr[(long long)c * ncols + n0];
+        gcnt[i] = (real + kBatch - 1) / kBatch * kBatch;
     }
 }
 
-// Scatter the +1 (SIGN=0) or -1 (SIGN=1) entries of columns
-// [col_begin, col_begin+ncols) to their merged position.  Position inside the
-// (chunk, column) bucket = rank among own-sign entries of the bucket + number
-// of opposite-sign entries of the bucket with a smaller row.
+__device__ __forceinline__ int lds_row_of(int c, int k_local) { return (c & 1) * kBufRows + k_local; }
+
+// Scatter the +1 (SIGN=0) or -1 (SIGN=1) entries to their stream slot.
+// Inside a (chunk, group) stream the columns follow each other and every
+// column's entries are in ascending row order (the +1/-1 lists merged), so
+// each output accumulates its nonzeros in ascending k.
 template <int SIGN>
 __global__ void k_scatter(const int* __restrict__ cs_own, const int* __restrict__ ri_own,
                           const int* __restrict__ cs_oth, const int* __restrict__ ri_oth,
                           const int* __restrict__ lb_own, const int* __restrict__ lb_oth,
-                          const int* __restrict__ cptr, int col_begin, int ncols, int tk,
-                          int* __restrict__ ent) {
+                          const int* __restrict__ cptr, const int* __restrict__ sptr, int col_begin, int ncols,
+                          int G, int2* __restrict__ ent) {
     const int base = cs_own[col_begin];
     const int total = cs_own[col_begin + ncols] - base;
+    const int sgn = SIGN ? (int)0xbf800000u : 0x3f800000;
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
         const int i = base + t;
-        // column: last n with cs_own[col_begin+n] <= i
-        int lo = 0, hi = ncols;  // answer in [0, ncols)
+        int lo = 0, hi = ncols;  // last n with cs_own[col_begin+n] <= i
         while (hi - lo > 1) {
-            int mid = (lo + hi) >> 1;
+            const int mid = (lo + hi) >> 1;
             if (cs_own[col_begin + mid] <= i) lo = mid; else hi = mid;
         }
         const int n = lo, gn = col_begin + n;
         const int k = ri_own[i];
-        const int c = k / tk;
+        const int c = k / kTK;
         const long long b = (long long)c * ncols + n;
+        const int g = n / kCW, j = n - g * kCW;
         const int rank_own = i - lb_own[b];
         const int rank_oth = lower_bound_i32(ri_oth, cs_oth[gn], cs_oth[gn + 1], k) - lb_oth[b];
-        const int pos = cptr[b] + rank_own + rank_oth;
-        ent[pos] = (k - c * tk) | (SIGN ? (int)0x80000000u : 0);
+        const int in_group = cptr[b] - cptr[(long long)c * ncols + g * kCW];
+        const int pos = sptr[(long long)c * G + g] + in_group + rank_own + rank_oth;
+        ent[pos] = make_int2(sgn, (lds_row_of(c, k - c * kTK) << 10) | (4 * j));
     }
 }
 
+// Padding entries: +1 x (the -0.0 row) -- an exact no-op on any accumulator.
+__global__ void k_fill_pads(const int* __restrict__ cptr, const int* __restrict__ sptr, int ncols, int nch, int G,
+                            int2* __restrict__ ent, long long n_entries) {
+    const long long total = (long long)nch * G;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int c = (int)(i / G), g = (int)(i % G);
+        const int n0 = g * kCW, n1 = min(n0 + kCW, ncols);
+        const int real = cptr[(long long)c * ncols + n1] - cptr[(long long)c * ncols + n0];
+        const int s0 = sptr[i], s1 = sptr[i + 1];
+        const int2 pad = make_int2(0x3f800000, lds_row_of(c, kTK) << 10);
+        for (int p = s0 + real; p < s1; ++p) ent[p] = pad;
+    }
+    // trailing guard batch (never consumed; keeps scalar loads in bounds)
+    if (blockIdx.x == 0 && threadIdx.x < kBatch) ent[n_entries + threadIdx.x] = make_int2(0x3f800000, kTK << 10);
+}
+
 // ---------------------------------------------------------------------------
-// The gather kernel
+// K1: the gather kernel
 // ---------------------------------------------------------------------------
 
-template <int TK>
-__device__ __forceinline__ void stage_x_tile(const float* __restrict__ X, int M, int K, int m0, int k0,
-                                             float2* __restrict__ xs, bool vec4) {
-    // Tile = 128 rows x TK k.  Work item = (row pair p, 4-wide k group q).
-    // Lanes run over 16 consecutive pairs first so the transposed LDS writes
-    // (xs[4q+j][p], 8 B each) from one 16-lane group hit 128 contiguous bytes.
-    constexpr int NQ = TK / 4;
-    constexpr int ITEMS = 64 * NQ;
-    for (int it = threadIdx.x; it < ITEMS; it += blockDim.x) {
-        const int p = (it & 15) | (((it >> 4) / NQ) << 4);
-        const int q = (it >> 4) % NQ;
-        const int r0 = m0 + 2 * p, r1 = r0 + 1;
-        const int kk = k0 + 4 * q;
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-        if (vec4 && kk + 3 < K) {
-            if (r0 < M) a = *reinterpret_cast<const float4*>(X + (size_t)r0 * K + kk);
-            if (r1 < M) b = *reinterpret_cast<const float4*>(X + (size_t)r1 * K + kk);
-        } else {
-            float va[4] = {0.f, 0.f, 0.f, 0.f}, vb[4] = {0.f, 0.f, 0.f, 0.f};
+// Transposed staging of X[m0..m0+255][k0..k0+63] into an LDS buffer laid out
+// [k][256 rows].  Each thread owns two 4x4 blocks (4 rows x 4 k): four
+// coalesced float4 loads (rows), a register transpose, four ds_write_b128
+// (k rows).  Lanes 0-7 of a wave own consecutive row quads so every 8-lane
+// write group stores 128 contiguous bytes (conflict-free), and per load
+// instruction the wave reads 8 rows x 128 B.
+struct Stage {
+    float4 v[2][4];
+};
+
+template <bool VEC4>
+__device__ __forceinline__ void stage_load(Stage& s, const float* __restrict__ X, int M, int K, int m0, int k0) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (kk + j < K) {
-                    if (r0 < M) va[j] = X[(size_t)r0 * K + kk + j];
-                    if (r1 < M) vb[j] = X[(size_t)r1 * K + kk + j];
+    for (int h = 0; h < 2; ++h) {
+        const int mq = (lane & 7) + 8 * w;        // 0..63
+        const int kq = (lane >> 3) + 8 * h;       // 0..15
+        const int kk = k0 + 4 * kq;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = m0 + 4 * mq + r;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (row < M) {
+                const float* src = X + (size_t)row * K + kk;
+                if (VEC4) {
+                    if (kk < K) v = *reinterpret_cast<const float4*>(src);  // K % 4 == 0
+                } else {
+                    if (kk + 0 < K) v.x = src[0];
+                    if (kk + 1 < K) v.y = src[1];
+                    if (kk + 2 < K) v.z = src[2];
+                    if (kk + 3 < K) v.w = src[3];
                 }
             }
-            a = make_float4(va[0], va[1], va[2], va[3]);
-            b = make_float4(vb[0], vb[1], vb[2], vb[3]);
+            s.v[h][r] = v;
         }
-        xs[(4 * q + 0) * 64 + p] = make_float2(a.x, b.x);
-        xs[(4 * q + 1) * 64 + p] = make_float2(a.y, b.y);
-        xs[(4 * q + 2) * 64 + p] = make_float2(a.z, b.z);
-        xs[(4 * q + 3) * 64 + p] = make_float2(a.w, b.w);
     }
 }
 
-// BIAS_FIRST: y = b; y +- x ...   (tcsc_sgemm_basic order, tcsc.c:74-96)
-// otherwise:  y = 0; y +- x ...; y += b   (prelu_basic order, tcsc.c:149-161)
-template <int TK, int CW, int WAVES, bool BIAS_FIRST, bool PRELU>
-__global__ void __launch_bounds__(WAVES * 64)
-k_tcsc_gather(const float* __restrict__ X, int M, int K,
-              const int* __restrict__ ent, const int* __restrict__ cptr, int ncols,
-              const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a, int vec4) {
-    __shared__ float2 xs[TK * 64];
+__device__ __forceinline__ void stage_store(const Stage& s, char* __restrict__ buf) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int mq = (lane & 7) + 8 * w;
+        const int kq = (lane >> 3) + 8 * h;
+        char* p = buf + (4 * kq) * kRowBytes + mq * 16;
+        *reinterpret_cast<float4*>(p + 0 * kRowBytes) = make_float4(s.v[h][0].x, s.v[h][1].x, s.v[h][2].x, s.v[h][3].x);
+        *reinterpret_cast<float4*>(p + 1 * kRowBytes) = make_float4(s.v[h][0].y, s.v[h][1].y, s.v[h][2].y, s.v[h][3].y);
+        *reinterpret_cast<float4*>(p + 2 * kRowBytes) = make_float4(s.v[h][0].z, s.v[h][1].z, s.v[h][2].z, s.v[h][3].z);
+        *reinterpret_cast<float4*>(p + 3 * kRowBytes) = make_float4(s.v[h][0].w, s.v[h][1].w, s.v[h][2].w, s.v[h][3].w);
+    }
+}
+
+// One 8-entry batch held in s[36:51] (A) or s[52:67] (B): address of entry i
+// = bfi(0x3ff, lane_off, word1) in v[200+i] -> ds_read_b128 into
+// v[168+4i : 171+4i].
+#define TCSC_ISSUE(S1, VA, V)                                                     \
+    "v_bfi_b32 " VA ", %[mask], %[lane], " S1 "\n\t"                              \
+    "ds_read_b128 " V ", " VA "\n\t"
+// acc[slot] += sign * x (exact): relative addressing of DST and SRC2 by 4*slot.
+#define TCSC_FMA(SLOT, SGN, X0, X1)                                               \
+    "s_set_gpr_idx_on " SLOT ", gpr_idx(SRC2,DST)\n\t"                            \
+    "v_pk_fma_f32 v[40:41], " X0 ", " SGN ", v[40:41] op_sel_hi:[1,0,1]\n\t"      \
+    "v_pk_fma_f32 v[42:43], " X1 ", " SGN ", v[42:43] op_sel_hi:[1,0,1]\n\t"      \
+    "s_set_gpr_idx_off\n\t"
+
+// Register names are spelled out per set: A = s36..s51, B = s52..s67.
+#define TCSC_ISSUE8_A                                                             \
+    TCSC_ISSUE("s37", "v200", "v[168:171]") TCSC_ISSUE("s39", "v201", "v[172:175]")               \
+    TCSC_ISSUE("s41", "v202", "v[176:179]") TCSC_ISSUE("s43", "v203", "v[180:183]")               \
+    TCSC_ISSUE("s45", "v204", "v[184:187]") TCSC_ISSUE("s47", "v205", "v[188:191]")               \
+    TCSC_ISSUE("s49", "v206", "v[192:195]") TCSC_ISSUE("s51", "v207", "v[196:199]")
+#define TCSC_ISSUE8_B                                                             \
+    TCSC_ISSUE("s53", "v200", "v[168:171]") TCSC_ISSUE("s55", "v201", "v[172:175]")               \
+    TCSC_ISSUE("s57", "v202", "v[176:179]") TCSC_ISSUE("s59", "v203", "v[180:183]")               \
+    TCSC_ISSUE("s61", "v204", "v[184:187]") TCSC_ISSUE("s63", "v205", "v[188:191]")               \
+    TCSC_ISSUE("s65", "v206", "v[192:195]") TCSC_ISSUE("s67", "v207", "v[196:199]")
+#define TCSC_FMA8_A                                                               \
+    TCSC_FMA("s37", "s[36:37]", "v[168:169]", "v[170:171]")                       \
+    TCSC_FMA("s39", "s[38:39]", "v[172:173]", "v[174:175]")                       \
+    TCSC_FMA("s41", "s[40:41]", "v[176:177]", "v[178:179]")                       \
+    TCSC_FMA("s43", "s[42:43]", "v[180:181]", "v[182:183]")                       \
+    TCSC_FMA("s45", "s[44:45]", "v[184:185]", "v[186:187]")                       \
+    TCSC_FMA("s47", "s[46:47]", "v[188:189]", "v[190:191]")                       \
+    TCSC_FMA("s49", "s[48:49]", "v[192:193]", "v[194:195]")                       \
+    TCSC_FMA("s51", "s[50:51]", "v[196:197]", "v[198:199]")
+#define TCSC_FMA8_B                                                               \
+    TCSC_FMA("s53", "s[52:53]", "v[168:169]", "v[170:171]")                       \
+    TCSC_FMA("s55", "s[54:55]", "v[172:173]", "v[174:175]")                       \
+    TCSC_FMA("s57", "s[56:57]", "v[176:177]", "v[178:179]")                       \
+    TCSC_FMA("s59", "s[58:59]", "v[180:181]", "v[182:183]")                       \
+    TCSC_FMA("s61", "s[60:61]", "v[184:185]", "v[186:187]")                       \
+    TCSC_FMA("s63", "s[62:63]", "v[188:189]", "v[190:191]")                       \
+    TCSC_FMA("s65", "s[64:65]", "v[192:193]", "v[194:195]")                       \
+    TCSC_FMA("s67", "s[66:67]", "v[196:197]", "v[198:199]")
+
+// Consume `nb` batches of this wave's stream starting at byte offset `off`
+// of `ent`.  M0 is written by s_set_gpr_idx_on; it is a reserved register
+// the compiler does not keep values in for this kernel (no LDS-DMA,
+// movrel or message instructions).  SMEM and LDS share lgkmcnt and SMEM returns out of order, so
+// every wait is lgkmcnt(0); the next batch's scalar load is issued once the
+// current batch's LDS data has landed and flies under its FMAs.
+__device__ __forceinline__ void gather_stream(const int2* __restrict__ ent, unsigned off, unsigned nb,
+                                              unsigned lane_off, unsigned mask, f32x32& a0, f32x32& a1,
+                                              f32x32& a2, f32x32& a3) {
+    asm volatile(
+        "s_cmp_eq_u32 %[nb], 0\n\t"
+        "s_cbranch_scc1 .Lend%=\n\t"
+        "s_load_dwordx16 s[36:51], %[ent], %[off]\n\t"
+        "s_add_u32 %[off], %[off], 64\n\t"
+        ".Ltop%=:\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        TCSC_ISSUE8_A
+        "s_sub_u32 %[nb], %[nb], 1\n\t"
+        "s_cmp_eq_u32 %[nb], 0\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_cbranch_scc1 .LlastA%=\n\t"
+        "s_load_dwordx16 s[52:67], %[ent], %[off]\n\t"
+        "s_add_u32 %[off], %[off], 64\n\t"
+        TCSC_FMA8_A
+        "s_waitcnt lgkmcnt(0)\n\t"
+        TCSC_ISSUE8_B
+        "s_sub_u32 %[nb], %[nb], 1\n\t"
+        "s_cmp_eq_u32 %[nb], 0\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_cbranch_scc1 .LlastB%=\n\t"
+        "s_load_dwordx16 s[36:51], %[ent], %[off]\n\t"
+        "s_add_u32 %[off], %[off], 64\n\t"
+        TCSC_FMA8_B
+        "s_branch .Ltop%=\n\t"
+        ".LlastA%=:\n\t"
+        TCSC_FMA8_A
+        "s_branch .Lend%=\n\t"
+        ".LlastB%=:\n\t"
+        TCSC_FMA8_B
+        ".Lend%=:\n\t"
+        : [off] "+s"(off), [nb] "+s"(nb), "+{v[40:71]}"(a0), "+{v[72:103]}"(a1), "+{v[104:135]}"(a2),
+          "+{v[136:167]}"(a3)
+        : [ent] "s"(ent), [lane] "v"(lane_off), [mask] "v"(mask)
+        : "memory", "scc", "v168", "v169", "v170", "v171", "v172", "v173", "v174", "v175", "v176", "v177",
+          "v178", "v179", "v180", "v181", "v182", "v183", "v184", "v185", "v186", "v187", "v188", "v189", "v190",
+          "v191", "v192", "v193", "v194", "v195", "v196", "v197", "v198", "v199", "v200", "v201", "v202", "v203", "v204", "v205", "v206", "v207", "s36", "s37", "s38",
+          "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53",
+          "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67");
+}
+
+// i is a compile-time constant after unrolling
+__device__ __forceinline__ float acc_get(const f32x32& a0, const f32x32& a1, const f32x32& a2, const f32x32& a3,
+                                         int i) {
+    return i < 32 ? a0[i] : (i < 64 ? a1[i - 32] : (i < 96 ? a2[i - 64] : a3[i - 96]));
+}
+__device__ __forceinline__ void acc_set(f32x32& a0, f32x32& a1, f32x32& a2, f32x32& a3, int i, float v) {
+    if (i < 32) a0[i] = v;
+    else if (i < 64) a1[i - 32] = v;
+    else if (i < 96) a2[i - 64] = v;
+    else a3[i - 96] = v;
+}
+
+// OUT: 0 = final Y (bias + activation), 1 = partial slab ws[slice][M][ncols]
+template <bool BIAS_FIRST, bool PRELU, bool VEC4, int OUT>
+__global__ void __launch_bounds__(kWaves * 64, 2)
+k_stream(const float* __restrict__ X, int M, int K, const int2* __restrict__ ent, const int* __restrict__ sptr,
+         int G, int ncols, int nch, int chunks_per_slice, const float* __restrict__ Bias, float* __restrict__ Y,
+         int ldy, float a, float* __restrict__ ws) {
+    __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int m0 = blockIdx.y * 128;
-    const int nw = (blockIdx.x * WAVES + wave) * CW;  // first column of this wave
-    const int nch = (K + TK - 1) / TK;
-    const int nvalid = min(CW, max(ncols - nw, 0));  // wave-uniform
+    const int g = blockIdx.x * kWaves + wave;  // wave-column group
+    const int m0 = blockIdx.y * kTM;
+    const int c_begin = blockIdx.z * chunks_per_slice;
+    const int c_end = min(nch, c_begin + chunks_per_slice);
+    const bool active = g < G;
 
-    float2 acc[CW];
+    f32x32 a0, a1, a2, a3;
 #pragma unroll
-    for (int j = 0; j < CW; ++j) {
-        float b0 = 0.f;
-        if (BIAS_FIRST && j < nvalid) b0 = Bias[nw + j];
-        acc[j] = make_float2(b0, b0);
+    for (int i = 0; i < 32; ++i) {
+        a0[i] = 0.f;
+        a1[i] = 0.f;
+        a2[i] = 0.f;
+        a3[i] = 0.f;
+    }
+    if (BIAS_FIRST && OUT == 0 && active) {
+#pragma unroll
+        for (int j = 0; j < kCW; ++j) {
+            const int col = g * kCW + j;
+            const float b = col < ncols ? Bias[col] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc_set(a0, a1, a2, a3, 4 * j + r, b);
+        }
     }
 
-    for (int c = 0; c < nch; ++c) {
-        if (c) __syncthreads();
-        stage_x_tile<TK>(X, M, K, m0, c * TK, xs, vec4 != 0);
+    // the -0.0 pad rows of both buffers (entries padding a stream point here)
+    if (threadIdx.x < 64) {
+        reinterpret_cast<float4*>(lds + kTK * kRowBytes)[threadIdx.x] = make_float4(-0.f, -0.f, -0.f, -0.f);
+        reinterpret_cast<float4*>(lds + (kBufRows + kTK) * kRowBytes)[threadIdx.x] =
+            make_float4(-0.f, -0.f, -0.f, -0.f);
+    }
+    Stage st;
+    if (c_begin < c_end) {
+        stage_load<VEC4>(st, X, M, K, m0, c_begin * kTK);
+        stage_store(st, lds + (c_begin & 1) * kBufRows * kRowBytes);
+    }
+    __syncthreads();
+
+    const unsigned lane_off = 16u * lane;
+    const unsigned mask = 0x3ffu;
+    for (int c = c_begin; c < c_end; ++c) {
+        const bool more = c + 1 < c_end;
+        if (more) stage_load<VEC4>(st, X, M, K, m0, (c + 1) * kTK);
+        if (active) {
+            const int s0 = sptr[(long long)c * G + g];
+            const int s1 = sptr[(long long)c * G + g + 1];
+            gather_stream(ent, (unsigned)s0 * 8u, (unsigned)(s1 - s0) / kBatch, lane_off, mask, a0, a1, a2, a3);
+        }
+        if (more) stage_store(st, lds + ((c + 1) & 1) * kBufRows * kRowBytes);
         __syncthreads();
-        if (nvalid == 0) continue;
-        const int* __restrict__ cp = cptr + (size_t)c * ncols + nw;
-        int p = cp[0];
+    }
+
+    if (!active) return;
 #pragma unroll
-        for (int j = 0; j < CW; ++j) {
-            if (j < nvalid) {
-                const int pe = cp[j + 1];
-                for (; p < pe; ++p) {
-                    const int e = ent[p];
-                    const float2 x = xs[(e & 0xffff) * 64 + lane];
-                    const float s = __int_as_float((e & (int)0x80000000u) | 0x3f800000);
-                    acc[j].x = __builtin_fmaf(x.x, s, acc[j].x);
-                    acc[j].y = __builtin_fmaf(x.y, s, acc[j].y);
+    for (int j = 0; j < kCW; ++j) {
+        const int col = g * kCW + j;
+        if (col < ncols) {
+            float b = 0.f;
+            if (OUT == 0 && !BIAS_FIRST) b = Bias[col];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = m0 + 4 * lane + r;
+                if (row < M) {
+                    float v = acc_get(a0, a1, a2, a3, 4 * j + r);
+                    if (OUT == 0) {
+                        if (!BIAS_FIRST) v += b;
+                        if (PRELU) v = (v < 0.0f) ? a * v : v;
+                        Y[(size_t)row * ldy + col] = v;
+                    } else {
+                        ws[((size_t)blockIdx.z * M + row) * ncols + col] = v;
+                    }
                 }
             }
         }
     }
+}
 
-    // epilogue
-    const int r0 = m0 + 2 * lane, r1 = r0 + 1;
-#pragma unroll
-    for (int j = 0; j < CW; ++j) {
-        if (j < nvalid) {
-            float y0 = acc[j].x, y1 = acc[j].y;
-            if (!BIAS_FIRST) {
-                const float b0 = Bias[nw + j];
-                y0 += b0;
-                y1 += b0;
-            }
-            if (PRELU) {
-                y0 = (y0 < 0.0f) ? a * y0 : y0;
-                y1 = (y1 < 0.0f) ? a * y1 : y1;
-            }
-            if (r0 < M) Y[(size_t)r0 * ldy + nw + j] = y0;
-            if (r1 < M) Y[(size_t)r1 * ldy + nw + j] = y1;
-        }
+// Split-K combine in slice order (deterministic): y = act(b + s0 + s1 ...)
+// or act(s0 + s1 + ... + b) depending on the variant's bias order.
+template <bool BIAS_FIRST, bool PRELU>
+__global__ void k_reduce(const float* __restrict__ ws, int slices, int M, int ncols, const float* __restrict__ Bias,
+                         float* __restrict__ Y, int ldy, float a) {
+    const long long total = (long long)M * ncols;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int row = (int)(i / ncols), col = (int)(i % ncols);
+        float v = BIAS_FIRST ? Bias[col] : 0.f;
+        for (int s = 0; s < slices; ++s) v += ws[(size_t)s * total + i];
+        if (!BIAS_FIRST) v += Bias[col];
+        if (PRELU) v = (v < 0.0f) ? a * v : v;
+        Y[(size_t)row * ldy + col] = v;
     }
 }
 
@@ -214,9 +408,8 @@ k_tcsc_gather(const float* __restrict__ X, int M, int K,
 // Device tcsc_from_dense (bit-exact with tcsc.c:6-66): per-column counts,
 // exclusive scans, then a fill that keeps rows ascending inside a column.
 // ---------------------------------------------------------------------------
-__global__ void k_dense_col_counts(const float* __restrict__ D, int rows, int cols,
-                                   int* __restrict__ cntp, int* __restrict__ cntn) {
-    // one thread per column; rows swept in order (coalesced across columns)
+__global__ void k_dense_col_counts(const float* __restrict__ D, int rows, int cols, int* __restrict__ cntp,
+                                   int* __restrict__ cntn) {
     for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < cols; n += gridDim.x * blockDim.x) {
         int p = 0, q = 0;
         for (int i = 0; i < rows; ++i) {
@@ -229,9 +422,8 @@ __global__ void k_dense_col_counts(const float* __restrict__ D, int rows, int co
     }
 }
 
-__global__ void k_dense_fill(const float* __restrict__ D, int rows, int cols,
-                             const int* __restrict__ csp, const int* __restrict__ csn,
-                             int* __restrict__ rip, int* __restrict__ rin) {
+__global__ void k_dense_fill(const float* __restrict__ D, int rows, int cols, const int* __restrict__ csp,
+                             const int* __restrict__ csn, int* __restrict__ rip, int* __restrict__ rin) {
     for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < cols; n += gridDim.x * blockDim.x) {
         int p = csp[n], q = csn[n];
         for (int i = 0; i < rows; ++i) {
@@ -253,79 +445,137 @@ static inline int grid_for(long long n, int block) {
     return (int)g;
 }
 
-hipError_t plan_build(const PlanDev& in, PlanOut& out, hipStream_t st) {
-    const int ncols = in.ncols, nch = out.n_chunks, tk = out.chunk_k;
-    const long long nb = (long long)(nch + 1) * ncols;
+hipError_t plan_scan_tmp_bytes(long long n, size_t* bytes) {
+    *bytes = 0;
+    return hipcub::DeviceScan::ExclusiveSum(nullptr, *bytes, (int*)nullptr, (int*)nullptr, (int)n, (hipStream_t)0);
+}
+
+// Phase 1: chunk bounds, per-(chunk, column) counts and their scan (cptr),
+// per-(chunk, group) padded stream lengths (gcnt, with a trailing 0).
+hipError_t plan_counts(const PlanDev& in, PlanOut& out, hipStream_t st) {
+    const int ncols = in.ncols, nch = out.n_chunks, G = out.n_groups;
     hipError_t e;
-    hipLaunchKernelGGL(k_chunk_bounds, dim3(grid_for(nb, 256)), dim3(256), 0, st, in.csp, in.csn,
-                       in.rip, in.rin, in.col_begin, ncols, nch, tk, in.rows, out.lbp, out.lbn);
+    const long long nb = (long long)(nch + 1) * ncols;
+    hipLaunchKernelGGL(k_chunk_bounds, dim3(grid_for(nb, 256)), dim3(256), 0, st, in.csp, in.csn, in.rip, in.rin,
+                       in.col_begin, ncols, nch, out.lbp, out.lbn);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const long long nc = (long long)nch * ncols;
-    hipLaunchKernelGGL(k_chunk_counts, dim3(grid_for(nc, 256)), dim3(256), 0, st, out.lbp, out.lbn,
-                       ncols, nch, out.cnt);
+    hipLaunchKernelGGL(k_chunk_counts, dim3(grid_for(nc, 256)), dim3(256), 0, st, out.lbp, out.lbn, ncols, nch,
+                       out.cnt);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    // cptr[i] = exclusive sum of cnt; cnt has one trailing 0 so cptr[nc] = nnz
-    size_t tmp_bytes = out.scan_tmp_bytes;
-    e = hipcub::DeviceScan::ExclusiveSum(out.scan_tmp, tmp_bytes, out.cnt, out.cptr, (int)(nc + 1), st);
-    if (e != hipSuccess) return e;
+    size_t tb = out.scan_tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(out.scan_tmp, tb, out.cnt, out.cptr, (int)(nc + 1), st)) != hipSuccess)
+        return e;
+    const long long ng = (long long)nch * G;
+    hipLaunchKernelGGL(k_group_counts, dim3(grid_for(ng, 256)), dim3(256), 0, st, out.cptr, ncols, nch, G, out.gcnt);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    tb = out.scan_tmp_bytes;
+    return hipcub::DeviceScan::ExclusiveSum(out.scan_tmp, tb, out.gcnt, out.sptr, (int)(ng + 1), st);
+}
+
+// Phase 2 (ent allocated with n_entries + kBatch): scatter + padding.
+hipError_t plan_fill(const PlanDev& in, PlanOut& out, hipStream_t st) {
+    const int ncols = in.ncols, nch = out.n_chunks, G = out.n_groups;
+    hipError_t e;
     if (in.n_pos > 0) {
-        hipLaunchKernelGGL(k_scatter<0>, dim3(grid_for(in.n_pos, 256)), dim3(256), 0, st, in.csp, in.rip,
-                           in.csn, in.rin, out.lbp, out.lbn, out.cptr, in.col_begin, ncols, tk, out.ent);
+        hipLaunchKernelGGL(k_scatter<0>, dim3(grid_for(in.n_pos, 256)), dim3(256), 0, st, in.csp, in.rip, in.csn,
+                           in.rin, out.lbp, out.lbn, out.cptr, out.sptr, in.col_begin, ncols, G, out.ent);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (in.n_neg > 0) {
-        hipLaunchKernelGGL(k_scatter<1>, dim3(grid_for(in.n_neg, 256)), dim3(256), 0, st, in.csn, in.rin,
-                           in.csp, in.rip, out.lbn, out.lbp, out.cptr, in.col_begin, ncols, tk, out.ent);
+        hipLaunchKernelGGL(k_scatter<1>, dim3(grid_for(in.n_neg, 256)), dim3(256), 0, st, in.csn, in.rin, in.csp,
+                           in.rip, out.lbn, out.lbp, out.cptr, out.sptr, in.col_begin, ncols, G, out.ent);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    return hipSuccess;
+    const long long ng = (long long)nch * G;
+    hipLaunchKernelGGL(k_fill_pads, dim3(grid_for(ng, 256)), dim3(256), 0, st, out.cptr, out.sptr, ncols, nch, G,
+                       out.ent, out.n_entries);
+    return hipGetLastError();
 }
 
-hipError_t plan_scan_tmp_bytes(long long n, size_t* bytes) {
-    *bytes = 0;
-    return hipcub::DeviceScan::ExclusiveSum(nullptr, *bytes, (int*)nullptr, (int*)nullptr, (int)n,
-                                            (hipStream_t)0);
+size_t workspace_bytes(int M, int ncols, int slices) {
+    return slices > 1 ? (size_t)slices * M * ncols * sizeof(float) : 0;
 }
 
-template <int TK, int CW, int WAVES>
-static hipError_t launch_gather_t(const GemmArgs& g, hipStream_t st) {
-    dim3 grid((g.ncols + WAVES * CW - 1) / (WAVES * CW), (g.M + 127) / 128);
-    dim3 block(WAVES * 64);
-    const int vec4 = (g.K % 4 == 0) && ((reinterpret_cast<uintptr_t>(g.X) & 15) == 0);
-    if (g.bias_first) {
-        if (g.prelu)
-            hipLaunchKernelGGL((k_tcsc_gather<TK, CW, WAVES, true, true>), grid, block, 0, st, g.X, g.M, g.K,
-                               g.ent, g.cptr, g.ncols, g.B, g.Y, g.ldy, g.a, vec4);
-        else
-            hipLaunchKernelGGL((k_tcsc_gather<TK, CW, WAVES, true, false>), grid, block, 0, st, g.X, g.M, g.K,
-                               g.ent, g.cptr, g.ncols, g.B, g.Y, g.ldy, g.a, vec4);
-    } else {
-        if (g.prelu)
-            hipLaunchKernelGGL((k_tcsc_gather<TK, CW, WAVES, false, true>), grid, block, 0, st, g.X, g.M, g.K,
-                               g.ent, g.cptr, g.ncols, g.B, g.Y, g.ldy, g.a, vec4);
-        else
-            hipLaunchKernelGGL((k_tcsc_gather<TK, CW, WAVES, false, false>), grid, block, 0, st, g.X, g.M, g.K,
-                               g.ent, g.cptr, g.ncols, g.B, g.Y, g.ldy, g.a, vec4);
+// Cost model (cycles of one CU at ~2.1 GHz) for k-slicing: every workgroup
+// runs on its own CU; gathers cost ~1 KiB / 220 B/clk per nonzero and
+// wave, staging ~1 KiB / 79 B/clk per k row (MI355X_MICROARCH.md LDS rows,
+// DESIGN.md measurements); the split-K slabs cost HBM time.
+int choose_slices(int M, int ncols, int K, long long nnz, int G, size_t ws_bytes, int force) {
+    const int nch = (K + kTK - 1) / kTK;
+    if (nch <= 1) return 1;
+    const int rt = (M + kTM - 1) / kTM;
+    const int cb = (G + kWaves - 1) / kWaves;
+    const long long base = (long long)rt * cb;
+    auto cap = [&](int s) { return s <= nch && workspace_bytes(M, ncols, s) <= ws_bytes; };
+    if (force > 0) return cap(force) ? force : 1;
+    const double nz_per_chunk_block = (double)nnz / nch / cb;  // per workgroup and chunk (all its waves)
+    const double chunk_cycles = nz_per_chunk_block * (1024.0 / 220.0) + kTK * (1024.0 / 79.0) + 600.0;
+    double best = 1e300;
+    int best_s = 1;
+    for (int s = 1; s <= 16; ++s) {
+        if (!cap(s)) break;
+        const long long blocks = base * s;
+        const long long rounds = (blocks + 255) / 256;
+        const int cps = (nch + s - 1) / s;
+        double t = (double)rounds * cps * chunk_cycles;
+        if (s > 1) t += (double)(s + 1) * M * ncols * 4.0 / 5.0e12 * 2.1e9 + 4000.0;
+        if (t < best * 0.97) {
+            best = t;
+            best_s = s;
+        }
     }
+    return best_s;
+}
+
+template <bool BF, bool PR>
+static hipError_t launch_t(const GemmArgs& g, int slices, bool vec4, hipStream_t st) {
+    const int nch = (g.K + kTK - 1) / kTK;
+    int cps = nch > 0 ? (nch + slices - 1) / slices : 1;
+    slices = nch > 0 ? (nch + cps - 1) / cps : 1;
+    dim3 grid((g.n_groups + kWaves - 1) / kWaves, (g.M + kTM - 1) / kTM, slices);
+    dim3 block(kWaves * 64);
+    if (slices == 1) {
+        if (vec4)
+            hipLaunchKernelGGL((k_stream<BF, PR, true, 0>), grid, block, 0, st, g.X, g.M, g.K, g.ent, g.sptr,
+                               g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
+        else
+            hipLaunchKernelGGL((k_stream<BF, PR, false, 0>), grid, block, 0, st, g.X, g.M, g.K, g.ent, g.sptr,
+                               g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
+        return hipGetLastError();
+    }
+    if (vec4)
+        hipLaunchKernelGGL((k_stream<BF, PR, true, 1>), grid, block, 0, st, g.X, g.M, g.K, g.ent, g.sptr, g.n_groups,
+                           g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
+    else
+        hipLaunchKernelGGL((k_stream<BF, PR, false, 1>), grid, block, 0, st, g.X, g.M, g.K, g.ent, g.sptr,
+                           g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const long long total = (long long)g.M * g.ncols;
+    hipLaunchKernelGGL((k_reduce<BF, PR>), dim3(grid_for(total, 256)), dim3(256), 0, st, g.ws, slices, g.M,
+                       g.ncols, g.B, g.Y, g.ldy, g.a);
     return hipGetLastError();
 }
 
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
     if (g.M <= 0 || g.ncols <= 0) return hipSuccess;
-    if (g.chunk_k != kChunkK) return hipErrorInvalidValue;
-    return launch_gather_t<kChunkK, 16, 4>(g, st);
+    const bool vec4 = (g.K % 4 == 0) && ((reinterpret_cast<uintptr_t>(g.X) & 15) == 0);
+    const int s = choose_slices(g.M, g.ncols, g.K, g.nnz, g.n_groups, g.ws ? g.ws_bytes : 0, g.force_slices);
+    if (g.bias_first) {
+        return g.prelu ? launch_t<true, true>(g, s, vec4, st) : launch_t<true, false>(g, s, vec4, st);
+    }
+    return g.prelu ? launch_t<false, true>(g, s, vec4, st) : launch_t<false, false>(g, s, vec4, st);
 }
 
 hipError_t dense_to_tcsc_counts(const float* D, int rows, int cols, int* cntp, int* cntn, hipStream_t st) {
-    hipLaunchKernelGGL(k_dense_col_counts, dim3(grid_for(cols, 256)), dim3(256), 0, st, D, rows, cols, cntp,
-                       cntn);
+    hipLaunchKernelGGL(k_dense_col_counts, dim3(grid_for(cols, 256)), dim3(256), 0, st, D, rows, cols, cntp, cntn);
     return hipGetLastError();
 }
 
-hipError_t dense_to_tcsc_fill(const float* D, int rows, int cols, const int* csp, const int* csn, int* rip,
-                              int* rin, hipStream_t st) {
-    hipLaunchKernelGGL(k_dense_fill, dim3(grid_for(cols, 256)), dim3(256), 0, st, D, rows, cols, csp, csn, rip,
-                       rin);
+hipError_t dense_to_tcsc_fill(const float* D, int rows, int cols, const int* csp, const int* csn, int* rip, int* rin,
+                              hipStream_t st) {
+    hipLaunchKernelGGL(k_dense_fill, dim3(grid_for(cols, 256)), dim3(256), 0, st, D, rows, cols, csp, csn, rip, rin);
     return hipGetLastError();
 }
 

@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_set_seed",
     # include/tcsc_gpu.h
     "tcsc_gpu_device_count", "tcsc_gpu_plan_create", "tcsc_gpu_plan_create_device", "tcsc_gpu_plan_get_info",
-    "tcsc_gpu_plan_destroy", "tcsc_gpu_sgemm", "tcsc_gpu_from_dense", "tcsc_gpu_last_error",
+    "tcsc_gpu_plan_reserve", "tcsc_gpu_plan_destroy", "tcsc_gpu_sgemm", "tcsc_gpu_from_dense", "tcsc_gpu_last_error",
     "tcsc_gpu_cache_clear", "tcsc_gpu_num_shards", "tcsc_gpu_set_num_shards",
 )
 
@@ -101,6 +101,7 @@ def lib():
     L.tcsc_gpu_plan_create.argtypes = [P, i, i, i, vp, C.POINTER(vp)]
     L.tcsc_gpu_plan_create_device.argtypes = [i, i, vp, vp, vp, vp, i, i, i, vp, C.POINTER(vp)]
     L.tcsc_gpu_plan_get_info.argtypes = [vp, C.POINTER(plan_info_t)]
+    L.tcsc_gpu_plan_reserve.argtypes = [vp, i]
     L.tcsc_gpu_plan_destroy.argtypes = [vp]
     L.tcsc_gpu_plan_destroy.restype = None
     L.tcsc_gpu_sgemm.argtypes = [vp, vp, vp, vp, i, i, i, f, vp]
@@ -250,6 +251,10 @@ class Plan:
         inf = plan_info_t()
         _check(lib().tcsc_gpu_plan_get_info(self.handle, C.byref(inf)), "tcsc_gpu_plan_get_info")
         return {k: getattr(inf, k) for k, _ in plan_info_t._fields_}
+
+    def reserve(self, max_M: int) -> None:
+        """Allocate the split-K workspace for launches of up to max_M rows."""
+        _check(lib().tcsc_gpu_plan_reserve(self.handle, int(max_M)), "tcsc_gpu_plan_reserve")
 
     def sgemm(self, X, B, Y, M: int, ldy: int, variant: str = "prelu_basic", a: float = 0.2,
               stream: int = 0) -> None:

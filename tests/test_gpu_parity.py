@@ -192,6 +192,7 @@ def run_device_cfg(torch, cfg, variant, x=None):
     tcsc_amd.gpu_from_dense(inp["Wd"], K, N, csp, csn, rip, rin)
     del inp["Wd"]
     plan = tcsc_amd.Plan.from_device(K, N, csp, csn, rip, rin)
+    plan.reserve(cfg.M)
     Y = torch.empty((cfg.M, N), device=dev)
     plan.sgemm(inp["X"], inp["B"], Y, cfg.M, N, variant, 0.2)
     torch.cuda.synchronize()
@@ -226,4 +227,39 @@ def test_baseline_config_sampled_rows(gpu, torch_cuda, oracle, cfg_idx):
     torch.cuda.synchronize()
     b = inp["B"].round()
     assert torch.equal(Yj - b, 2 * (Yi - b))
+    plan.destroy()
+
+
+@pytest.mark.parametrize("slices", [2, 3, 7])
+def test_split_k_paths(gpu, torch_cuda, oracle, monkeypatch, slices):
+    """k-sliced launches (partial slabs + ordered reduce) against the oracle:
+    integer inputs must be bit-identical, float within tolerance."""
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    M, K, N = 300, 1500, 200
+    Wd = oracle.ternary((K, N), 0.05, 21)
+    W = oracle.tcsc_from_dense(Wd)
+    Wm = tcsc_amd.TcscMatrix.from_dense(Wd)
+    plan = tcsc_amd.Plan(Wm)
+    monkeypatch.setenv("TCSC_SLICES", str(slices))
+    plan.reserve(M)
+    Xi = oracle.integers((M, K), 22)
+    Bi = oracle.integers((N,), 23)
+    for variant in ("basic", "prelu_basic"):
+        dY = torch.empty((M, N), device=dev)
+        plan.sgemm(torch.from_numpy(Xi).to(dev), torch.from_numpy(Bi).to(dev), dY, M, N, variant, 0.25)
+        torch.cuda.synchronize()
+        ref = oracle.sgemm(variant, Xi, W, Bi, 0.25)
+        np.testing.assert_array_equal(dY.cpu().numpy(), ref)
+    X = oracle.uniform((M, K), 24)
+    B = oracle.uniform((N,), 25)
+    dY = torch.empty((M, N), device=dev)
+    plan.sgemm(torch.from_numpy(X).to(dev), torch.from_numpy(B).to(dev), dY, M, N, "prelu_onthego", 0.2)
+    torch.cuda.synchronize()
+    Y64, S64 = oracle.f64_rows(X, W, B)
+    ok, ratio = pyoracle.check_close(dY.cpu().numpy(), Y64, S64, 0.2)
+    assert ok, ratio
+    # host API with the same forced split
+    Yh = tcsc_amd.sgemm("basic", Xi, Wm, Bi)
+    np.testing.assert_array_equal(Yh, oracle.sgemm("basic", Xi, W, Bi))
     plan.destroy()
