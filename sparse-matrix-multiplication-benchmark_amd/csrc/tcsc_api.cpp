@@ -110,10 +110,10 @@ int build_plan(int rows, int col_begin, int ncols, long long n_pos, long long n_
     HIP_TRY(hipMalloc(&plan->sptr, (size_t)(ng + 1) * sizeof(int)));
     if (ng == 0) {
         HIP_TRY(hipMemsetAsync(plan->sptr, 0, sizeof(int), st));
-        HIP_TRY(hipMalloc(&plan->ent, tcsc::kBatch * sizeof(int2)));
-        HIP_TRY(hipMemsetAsync(plan->ent, 0, tcsc::kBatch * sizeof(int2), st));
+        HIP_TRY(hipMalloc(&plan->ent, tcsc::kEntGuard * sizeof(int2)));
+        HIP_TRY(hipMemsetAsync(plan->ent, 0, tcsc::kEntGuard * sizeof(int2), st));
         HIP_TRY(hipStreamSynchronize(st));
-        plan->bytes = sizeof(int) + tcsc::kBatch * sizeof(int2);
+        plan->bytes = sizeof(int) + tcsc::kEntGuard * sizeof(int2);
         *out = plan.release();
         return TCSC_OK;
     }
@@ -157,11 +157,11 @@ int build_plan(int rows, int col_begin, int ncols, long long n_pos, long long n_
     HIP_TRY(hipStreamSynchronize(st));
     po.n_entries = total;
     plan->n_entries = total;
-    HIP_TRY(hipMalloc(&plan->ent, (size_t)(total + tcsc::kBatch) * sizeof(int2)));
+    HIP_TRY(hipMalloc(&plan->ent, (size_t)(total + tcsc::kEntGuard) * sizeof(int2)));
     po.ent = plan->ent;
     HIP_TRY(tcsc::plan_fill(in, po, st));
     HIP_TRY(hipStreamSynchronize(st));
-    plan->bytes = (size_t)(ng + 1) * sizeof(int) + (size_t)(total + tcsc::kBatch) * sizeof(int2);
+    plan->bytes = (size_t)(ng + 1) * sizeof(int) + (size_t)(total + tcsc::kEntGuard) * sizeof(int2);
     *out = plan.release();
     return TCSC_OK;
 }

@@ -13,7 +13,8 @@ constexpr int kRowBytes = kTM * 4;       // one LDS row = X[m0..m0+255][k], 1 Ki
 constexpr int kBufRows = kTK + 1;        // + one row of -0.0 that padding entries point at
 constexpr int kWaves = 8;                // waves per workgroup (1 workgroup per CU)
 constexpr int kCW = 32;                  // output columns per wave (4*kCW accumulator VGPRs)
-constexpr int kBatch = 8;                // stream entries per s_load_dwordx16
+constexpr int kBatch = 8;                // stream entries per batch (pipeline step)
+constexpr int kEntGuard = 64;            // entries allocated past the last stream (block loads)
 constexpr int kLdsBytes = 2 * kBufRows * kRowBytes;  // double-buffered tile: 130 KiB
 
 // Stream entry (8 bytes): word0 = +1.0f or -1.0f (bit pattern), word1 =

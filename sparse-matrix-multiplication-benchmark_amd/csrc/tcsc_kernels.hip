@@ -137,8 +137,8 @@ __global__ void k_fill_pads(const int* __restrict__ cptr, const int* __restrict_
         const int2 pad = make_int2(0x3f800000, lds_row_of(c, kTK) << 10);
         for (int p = s0 + real; p < s1; ++p) ent[p] = pad;
     }
-    // trailing guard batch (never consumed; keeps scalar loads in bounds)
-    if (blockIdx.x == 0 && threadIdx.x < kBatch) ent[n_entries + threadIdx.x] = make_int2(0x3f800000, kTK << 10);
+    // trailing guard block (never consumed; keeps the 64-entry block loads in bounds)
+    if (blockIdx.x == 0 && threadIdx.x < kEntGuard) ent[n_entries + threadIdx.x] = make_int2(0x3f800000, kTK << 10);
 }
 
 // ---------------------------------------------------------------------------
@@ -155,30 +155,41 @@ struct Stage {
     float4 v[2][4];
 };
 
+// Branch-free and select-free loads, so all eight issue back to back and are
+// waited for once, at stage_store.  Values staged for rows >= M or k >= K are
+// never used (no stream entry points at a k row past K, and rows past M are
+// not stored), so only memory safety matters: VEC4 (K % 4 == 0, X 16-B
+// aligned, (M+256)*K*4 < 2^31) uses raw buffer loads, whose range check
+// returns 0 past the end of X; one 32-bit offset VGPR per row keeps address
+// registers few, so the staged tile stays out of the registers the gather
+// asm owns.  Otherwise clamped scalar loads.
 template <bool VEC4>
 __device__ __forceinline__ void stage_load(Stage& s, const float* __restrict__ X, int M, int K, int m0, int k0) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int mq = (lane & 7) + 8 * w;  // 0..63
+    if (VEC4) {
+        const __amdgpu_buffer_rsrc_t rsrc =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X), (short)0, M * K * 4, 0x00020000);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int kk = k0 + 4 * ((lane >> 3) + 8 * h);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const unsigned off = (unsigned)((m0 + 4 * mq + r) * K + kk) * 4u;
+                s.v[h][r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        const int mq = (lane & 7) + 8 * w;        // 0..63
-        const int kq = (lane >> 3) + 8 * h;       // 0..15
-        const int kk = k0 + 4 * kq;
+        const int kk = k0 + 4 * ((lane >> 3) + 8 * h);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int row = m0 + 4 * mq + r;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (row < M) {
-                const float* src = X + (size_t)row * K + kk;
-                if (VEC4) {
-                    if (kk < K) v = *reinterpret_cast<const float4*>(src);  // K % 4 == 0
-                } else {
-                    if (kk + 0 < K) v.x = src[0];
-                    if (kk + 1 < K) v.y = src[1];
-                    if (kk + 2 < K) v.z = src[2];
-                    if (kk + 3 < K) v.w = src[3];
-                }
-            }
-            s.v[h][r] = v;
+            const int row = min(m0 + 4 * mq + r, M - 1);
+            const float* src = X + (size_t)row * K;
+            s.v[h][r] = make_float4(src[min(kk, K - 1)], src[min(kk + 1, K - 1)], src[min(kk + 2, K - 1)],
+                                    src[min(kk + 3, K - 1)]);
         }
     }
 }
@@ -197,97 +208,30 @@ __device__ __forceinline__ void stage_store(const Stage& s, char* __restrict__ b
     }
 }
 
-// One 8-entry batch held in s[36:51] (A) or s[52:67] (B): address of entry i
-// = bfi(0x3ff, lane_off, word1) in v[200+i] -> ds_read_b128 into
-// v[168+4i : 171+4i].
-#define TCSC_ISSUE(S1, VA, V)                                                     \
-    "v_bfi_b32 " VA ", %[mask], %[lane], " S1 "\n\t"                              \
-    "ds_read_b128 " V ", " VA "\n\t"
-// acc[slot] += sign * x (exact): relative addressing of DST and SRC2 by 4*slot.
-#define TCSC_FMA(SLOT, SGN, X0, X1)                                               \
-    "s_set_gpr_idx_on " SLOT ", gpr_idx(SRC2,DST)\n\t"                            \
-    "v_pk_fma_f32 v[40:41], " X0 ", " SGN ", v[40:41] op_sel_hi:[1,0,1]\n\t"      \
-    "v_pk_fma_f32 v[42:43], " X1 ", " SGN ", v[42:43] op_sel_hi:[1,0,1]\n\t"      \
-    "s_set_gpr_idx_off\n\t"
+#include "gather_asm.inc"
 
-// Register names are spelled out per set: A = s36..s51, B = s52..s67.
-#define TCSC_ISSUE8_A                                                             \
-    TCSC_ISSUE("s37", "v200", "v[168:171]") TCSC_ISSUE("s39", "v201", "v[172:175]")               \
-    TCSC_ISSUE("s41", "v202", "v[176:179]") TCSC_ISSUE("s43", "v203", "v[180:183]")               \
-    TCSC_ISSUE("s45", "v204", "v[184:187]") TCSC_ISSUE("s47", "v205", "v[188:191]")               \
-    TCSC_ISSUE("s49", "v206", "v[192:195]") TCSC_ISSUE("s51", "v207", "v[196:199]")
-#define TCSC_ISSUE8_B                                                             \
-    TCSC_ISSUE("s53", "v200", "v[168:171]") TCSC_ISSUE("s55", "v201", "v[172:175]")               \
-    TCSC_ISSUE("s57", "v202", "v[176:179]") TCSC_ISSUE("s59", "v203", "v[180:183]")               \
-    TCSC_ISSUE("s61", "v204", "v[184:187]") TCSC_ISSUE("s63", "v205", "v[188:191]")               \
-    TCSC_ISSUE("s65", "v206", "v[192:195]") TCSC_ISSUE("s67", "v207", "v[196:199]")
-#define TCSC_FMA8_A                                                               \
-    TCSC_FMA("s37", "s[36:37]", "v[168:169]", "v[170:171]")                       \
-    TCSC_FMA("s39", "s[38:39]", "v[172:173]", "v[174:175]")                       \
-    TCSC_FMA("s41", "s[40:41]", "v[176:177]", "v[178:179]")                       \
-    TCSC_FMA("s43", "s[42:43]", "v[180:181]", "v[182:183]")                       \
-    TCSC_FMA("s45", "s[44:45]", "v[184:185]", "v[186:187]")                       \
-    TCSC_FMA("s47", "s[46:47]", "v[188:189]", "v[190:191]")                       \
-    TCSC_FMA("s49", "s[48:49]", "v[192:193]", "v[194:195]")                       \
-    TCSC_FMA("s51", "s[50:51]", "v[196:197]", "v[198:199]")
-#define TCSC_FMA8_B                                                               \
-    TCSC_FMA("s53", "s[52:53]", "v[168:169]", "v[170:171]")                       \
-    TCSC_FMA("s55", "s[54:55]", "v[172:173]", "v[174:175]")                       \
-    TCSC_FMA("s57", "s[56:57]", "v[176:177]", "v[178:179]")                       \
-    TCSC_FMA("s59", "s[58:59]", "v[180:181]", "v[182:183]")                       \
-    TCSC_FMA("s61", "s[60:61]", "v[184:185]", "v[186:187]")                       \
-    TCSC_FMA("s63", "s[62:63]", "v[188:189]", "v[190:191]")                       \
-    TCSC_FMA("s65", "s[64:65]", "v[192:193]", "v[194:195]")                       \
-    TCSC_FMA("s67", "s[66:67]", "v[196:197]", "v[198:199]")
-
-// Consume `nb` batches of this wave's stream starting at byte offset `off`
-// of `ent`.  M0 is written by s_set_gpr_idx_on; it is a reserved register
-// the compiler does not keep values in for this kernel (no LDS-DMA,
-// movrel or message instructions).  SMEM and LDS share lgkmcnt and SMEM returns out of order, so
-// every wait is lgkmcnt(0); the next batch's scalar load is issued once the
-// current batch's LDS data has landed and flies under its FMAs.
-__device__ __forceinline__ void gather_stream(const int2* __restrict__ ent, unsigned off, unsigned nb,
+// Consume this wave's stream for one chunk: `nb` batches of 8 entries at
+// `stream` (entries padded to a multiple of 8; the first 64-entry block is
+// already in e_sgn/e_w1, lane i = entry i).  The schedule and register map
+// are in tools/gen_gather_asm.py.  M0 is written by s_set_gpr_idx_*; it is a
+// reserved register the compiler keeps nothing in for this kernel (no
+// LDS-DMA, movrel or message instructions).
+__device__ __forceinline__ void gather_stream(const int2* __restrict__ stream, unsigned nb, int e_sgn, int e_w1,
                                               unsigned lane_off, unsigned mask, f32x32& a0, f32x32& a1,
                                               f32x32& a2, f32x32& a3) {
-    asm volatile(
-        "s_cmp_eq_u32 %[nb], 0\n\t"
-        "s_cbranch_scc1 .Lend%=\n\t"
-        "s_load_dwordx16 s[36:51], %[ent], %[off]\n\t"
-        "s_add_u32 %[off], %[off], 64\n\t"
-        ".Ltop%=:\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        TCSC_ISSUE8_A
-        "s_sub_u32 %[nb], %[nb], 1\n\t"
-        "s_cmp_eq_u32 %[nb], 0\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "s_cbranch_scc1 .LlastA%=\n\t"
-        "s_load_dwordx16 s[52:67], %[ent], %[off]\n\t"
-        "s_add_u32 %[off], %[off], 64\n\t"
-        TCSC_FMA8_A
-        "s_waitcnt lgkmcnt(0)\n\t"
-        TCSC_ISSUE8_B
-        "s_sub_u32 %[nb], %[nb], 1\n\t"
-        "s_cmp_eq_u32 %[nb], 0\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "s_cbranch_scc1 .LlastB%=\n\t"
-        "s_load_dwordx16 s[36:51], %[ent], %[off]\n\t"
-        "s_add_u32 %[off], %[off], 64\n\t"
-        TCSC_FMA8_B
-        "s_branch .Ltop%=\n\t"
-        ".LlastA%=:\n\t"
-        TCSC_FMA8_A
-        "s_branch .Lend%=\n\t"
-        ".LlastB%=:\n\t"
-        TCSC_FMA8_B
-        ".Lend%=:\n\t"
-        : [off] "+s"(off), [nb] "+s"(nb), "+{v[40:71]}"(a0), "+{v[72:103]}"(a1), "+{v[104:135]}"(a2),
-          "+{v[136:167]}"(a3)
-        : [ent] "s"(ent), [lane] "v"(lane_off), [mask] "v"(mask)
-        : "memory", "scc", "v168", "v169", "v170", "v171", "v172", "v173", "v174", "v175", "v176", "v177",
-          "v178", "v179", "v180", "v181", "v182", "v183", "v184", "v185", "v186", "v187", "v188", "v189", "v190",
-          "v191", "v192", "v193", "v194", "v195", "v196", "v197", "v198", "v199", "v200", "v201", "v202", "v203", "v204", "v205", "v206", "v207", "s36", "s37", "s38",
-          "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53",
-          "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67");
+    unsigned voff = (lane_off >> 4) * 8u;  // byte offset of this lane's entry in a block
+    asm volatile(TCSC_GATHER_ASM
+                 : [nb] "+s"(nb), "+{v[40:71]}"(a0), "+{v[72:103]}"(a1), "+{v[104:135]}"(a2),
+                   "+{v[136:167]}"(a3), "+{v232}"(e_sgn), "+{v233}"(e_w1), "+{v236}"(voff)
+                 : [ent] "s"(stream), [lane] "v"(lane_off), [mask] "v"(mask)
+                 : "memory", "scc", "v168", "v169", "v170", "v171", "v172", "v173", "v174", "v175", "v176",
+                   "v177", "v178", "v179", "v180", "v181", "v182", "v183", "v184", "v185", "v186", "v187", "v188",
+                   "v189", "v190", "v191", "v192", "v193", "v194", "v195", "v196", "v197", "v198", "v199", "v200",
+                   "v201", "v202", "v203", "v204", "v205", "v206", "v207", "v208", "v209", "v210", "v211", "v212",
+                   "v213", "v214", "v215", "v216", "v217", "v218", "v219", "v220", "v221", "v222", "v223", "v224",
+                   "v225", "v226", "v227", "v228", "v229", "v230", "v231", "v234", "v235", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43",
+                   "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57",
+                   "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67");
 }
 
 // i is a compile-time constant after unrolling
@@ -326,10 +270,13 @@ k_stream(const float* __restrict__ X, int M, int K, const int2* __restrict__ ent
         a3[i] = 0.f;
     }
     if (BIAS_FIRST && OUT == 0 && active) {
+        // one vector load of the wave's 32 bias values, then lane broadcasts
+        // (keeps them out of the SGPRs the gather loop owns)
+        const int cb = g * kCW + (lane & (kCW - 1));
+        const float bv = cb < ncols ? Bias[cb] : 0.f;
 #pragma unroll
         for (int j = 0; j < kCW; ++j) {
-            const int col = g * kCW + j;
-            const float b = col < ncols ? Bias[col] : 0.f;
+            const float b = __shfl(bv, j);
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc_set(a0, a1, a2, a3, 4 * j + r, b);
         }
@@ -350,15 +297,44 @@ k_stream(const float* __restrict__ X, int M, int K, const int2* __restrict__ ent
 
     const unsigned lane_off = 16u * lane;
     const unsigned mask = 0x3ffu;
+    // Software-pipelined chunk loop.  Stream bounds come 64 chunks at a time
+    // (lane i = chunk cb+i) and are read with readlane; the first entry block
+    // of chunk c+1 is loaded during chunk c, before the staging loads, so the
+    // gather's input was issued a whole chunk earlier.  No branches around
+    // the loads: staging the chunk after the last one and streams of idle
+    // waves are harmless (clamped reads, nb = 0, an LDS buffer nobody reads).
+    const int gi = active ? g : G - 1;
+    int cb = c_begin;
+    int vs0 = 0, vs1 = 0;
+    int2 en = make_int2(0, 0);
+    int s0n = 0, s1n = 0;
+    if (c_begin < c_end) {
+        const long long ci = (long long)min(cb + lane, nch - 1) * G + gi;
+        vs0 = sptr[ci];
+        vs1 = sptr[ci + 1];
+        s0n = __builtin_amdgcn_readlane(vs0, 0);
+        s1n = __builtin_amdgcn_readlane(vs1, 0);
+        en = ent[s0n + lane];
+    }
     for (int c = c_begin; c < c_end; ++c) {
-        const bool more = c + 1 < c_end;
-        if (more) stage_load<VEC4>(st, X, M, K, m0, (c + 1) * kTK);
-        if (active) {
-            const int s0 = sptr[(long long)c * G + g];
-            const int s1 = sptr[(long long)c * G + g + 1];
-            gather_stream(ent, (unsigned)s0 * 8u, (unsigned)(s1 - s0) / kBatch, lane_off, mask, a0, a1, a2, a3);
+        const int s0 = s0n, s1 = s1n;
+        const int2 e = en;
+        int idx = c + 1 - cb;
+        if (idx == 64) {
+            cb += 64;
+            idx = 0;
+            const long long ci = (long long)min(cb + lane, nch - 1) * G + gi;
+            vs0 = sptr[ci];
+            vs1 = sptr[ci + 1];
         }
-        if (more) stage_store(st, lds + ((c + 1) & 1) * kBufRows * kRowBytes);
+        s0n = __builtin_amdgcn_readlane(vs0, idx);
+        s1n = __builtin_amdgcn_readlane(vs1, idx);
+        en = ent[s0n + lane];
+        asm volatile("" ::: "memory");  // keep the entry load ahead of the staging loads
+        stage_load<VEC4>(st, X, M, K, m0, (c + 1) * kTK);
+        const unsigned nb = active ? (unsigned)(s1 - s0) / kBatch : 0u;
+        gather_stream(ent + s0, nb, e.x, e.y, lane_off, mask, a0, a1, a2, a3);
+        stage_store(st, lds + ((c + 1) & 1) * kBufRows * kRowBytes);
         __syncthreads();
     }
 
@@ -560,7 +536,8 @@ static hipError_t launch_t(const GemmArgs& g, int slices, bool vec4, hipStream_t
 
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
     if (g.M <= 0 || g.ncols <= 0) return hipSuccess;
-    const bool vec4 = (g.K % 4 == 0) && ((reinterpret_cast<uintptr_t>(g.X) & 15) == 0);
+    const bool vec4 = (g.K % 4 == 0) && ((reinterpret_cast<uintptr_t>(g.X) & 15) == 0) &&
+                      ((long long)(g.M + kTM) * g.K * 4 < (1LL << 31));
     const int s = choose_slices(g.M, g.ncols, g.K, g.nnz, g.n_groups, g.ws ? g.ws_bytes : 0, g.force_slices);
     if (g.bias_first) {
         return g.prelu ? launch_t<true, true>(g, s, vec4, st) : launch_t<true, false>(g, s, vec4, st);

@@ -93,6 +93,7 @@ def test_device_api_matches_host_api(gpu, torch_cuda, oracle):
     M, N = g["X"].shape[0], W.cols
     stream = torch.cuda.current_stream().cuda_stream
     plan = tcsc_amd.Plan(W, 0, N, 0, stream)
+    plan.reserve(M)  # same split-K choice as the host API
     for variant in pyoracle.VARIANTS:
         Yd = torch.full((M, N + 7), 123.0, device=dev)  # ldy > N: padding untouched
         plan.sgemm(X, B, Yd, M, N + 7, variant, float(g["a"]), stream)
