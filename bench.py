@@ -53,6 +53,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--override", default="", help="experiments only: e.g. 'K=16448,N=4096' (marks the line)")
     return p.parse_args()
 
 
@@ -79,6 +80,11 @@ def main():
     tcsc_amd.require_gpu()
 
     cfg = workloads.CONFIGS[args.config]
+    if args.override:
+        import dataclasses
+
+        kv = dict(x.split("=") for x in args.override.split(","))
+        cfg = dataclasses.replace(cfg, **{k: (float(v) if k == "sparsity" else int(v)) for k, v in kv.items()})
     variant = args.variant or cfg.variant
     # this rank's column block
     if args.scaling == "weak":
@@ -169,7 +175,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic (X,B ~ U[-1,1), W iid ternary; seeded torch generators)",
             "config": {
-                "workload": f"{cfg.name}: {cfg.describe()}",
+                "workload": f"{cfg.name}: {cfg.describe()}" + (f" [override {args.override}]" if args.override else ""),
                 "M": cfg.M, "K": cfg.K, "N": cfg.N, "sparsity": cfg.sparsity, "variant": variant,
                 "columns_per_gpu": ncols, "nnz_per_gpu": nnz,
                 "parallelism": f"column-shard x{world} ({args.scaling}), no collective",

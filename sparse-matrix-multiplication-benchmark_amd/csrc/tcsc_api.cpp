@@ -172,10 +172,11 @@ int slices_override() {
     return s ? std::atoi(s) : 0;
 }
 
+// Workspace of one call = [X^T: xt_bytes(M, K)] [split-K slabs, if any].
 size_t wanted_workspace(const tcsc_gpu_plan* p, int M) {
     const int s = tcsc::choose_slices(M, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
                                       slices_override());
-    return tcsc::workspace_bytes(M, p->cols, s);
+    return tcsc::xt_bytes(M, p->rows) + tcsc::workspace_bytes(M, p->cols, s);
 }
 
 class DeviceGuard {
@@ -208,8 +209,14 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
         set_error("tcsc_gpu_sgemm: NULL device pointer");
         return TCSC_E_ARG;
     }
+    const size_t xtb = tcsc::xt_bytes(M, p->rows);
+    if (p->rows > 0 && (!ws || ws_bytes < xtb)) {
+        set_error("tcsc_gpu_sgemm: workspace of %zu bytes < %zu needed for M=%d", ws ? ws_bytes : (size_t)0, xtb, M);
+        return TCSC_E_ARG;
+    }
     tcsc::GemmArgs g;
     g.X = dX;
+    g.XT = p->rows > 0 ? ws : nullptr;
     g.M = M;
     g.K = p->rows;
     g.ent = p->ent;
@@ -221,8 +228,8 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
     g.Y = dY;
     g.ldy = ldy;
     g.a = a;
-    g.ws = ws;
-    g.ws_bytes = ws ? ws_bytes : 0;
+    g.ws = (ws && ws_bytes > xtb) ? reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + xtb) : nullptr;
+    g.ws_bytes = g.ws ? ws_bytes - xtb : 0;
     g.force_slices = slices_override();
     // Bias first for tcsc_sgemm_basic (tcsc.c:74-96), last otherwise
     // (tcsc.c:149-161; the optimized family adds per-sign partial sums to
@@ -344,7 +351,10 @@ int tcsc_gpu_plan_reserve(tcsc_gpu_plan* p, int max_M) {
     const size_t want = wanted_workspace(p, max_M);
     if (want <= p->ws_bytes) return TCSC_OK;
     DeviceGuard dg(p->device);
-    if (p->ws) (void)hipFree(p->ws);
+    if (p->ws) {
+        HIP_TRY(hipDeviceSynchronize());  // a queued launch may still use it
+        (void)hipFree(p->ws);
+    }
     p->ws = nullptr;
     p->ws_bytes = 0;
     HIP_TRY(hipMalloc(&p->ws, want));
@@ -355,6 +365,12 @@ int tcsc_gpu_plan_reserve(tcsc_gpu_plan* p, int max_M) {
 
 int tcsc_gpu_sgemm(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy,
                    int variant, float a, void* stream) {
+    // grow the workspace on first use at a larger M (tcsc_gpu_plan_reserve
+    // up front keeps this call allocation-free and graph-capturable)
+    if (p && M > 0 && p->cols > 0 && p->ws_bytes < wanted_workspace(p, M)) {
+        const int rc = tcsc_gpu_plan_reserve(const_cast<tcsc_gpu_plan*>(p), M);
+        if (rc != TCSC_OK) return rc;
+    }
     return sgemm_ws(p, dX, dB, dY, M, ldy, variant, a, stream, p ? p->ws : nullptr, p ? p->ws_bytes : 0);
 }
 

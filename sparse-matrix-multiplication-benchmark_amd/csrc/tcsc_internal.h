@@ -8,17 +8,28 @@ namespace tcsc {
 
 // ---- geometry of the gather kernel (DESIGN.md "Kernel K1") ---------------
 constexpr int kTM = 256;                 // rows per workgroup: 64 lanes x 4 rows (ds_read_b128)
-constexpr int kTK = 64;                  // K rows per LDS chunk
+#ifndef TCSC_TK
+#define TCSC_TK 48
+#endif
+#ifndef TCSC_NBUF
+#define TCSC_NBUF 3
+#endif
+constexpr int kTK = TCSC_TK;             // K rows per LDS chunk
+constexpr int kNBuf = TCSC_NBUF;         // LDS tile ring: chunk c in buffer c % kNBuf, kNBuf-1 chunks in flight
 constexpr int kRowBytes = kTM * 4;       // one LDS row = X[m0..m0+255][k], 1 KiB
 constexpr int kBufRows = kTK + 1;        // + one row of -0.0 that padding entries point at
 constexpr int kWaves = 8;                // waves per workgroup (1 workgroup per CU)
 constexpr int kCW = 32;                  // output columns per wave (4*kCW accumulator VGPRs)
 constexpr int kBatch = 8;                // stream entries per batch (pipeline step)
 constexpr int kEntGuard = 64;            // entries allocated past the last stream (block loads)
-constexpr int kLdsBytes = 2 * kBufRows * kRowBytes;  // double-buffered tile: 130 KiB
+constexpr int kLdsBytes = kNBuf * kBufRows * kRowBytes;  // 147 KiB
+constexpr int kDmaPerWave = kTK / kWaves;                 // 1-KiB LDS-DMA rows per wave and chunk
+static_assert(kTK % kWaves == 0, "each wave DMAs the same number of rows");
+static_assert(kLdsBytes <= 160 * 1024, "LDS");
+static_assert(kNBuf == 3, "k_stream issues DMA(c+2) into the buffer chunk c-1 used");
 
 // Stream entry (8 bytes): word0 = +1.0f or -1.0f (bit pattern), word1 =
-// (lds_row << 10) | (4*slot); lds_row = (chunk&1)*kBufRows + (k - chunk*kTK)
+// (lds_row << 10) | (4*slot); lds_row = (chunk%3)*kBufRows + (k - chunk*kTK)
 // or the pad row; slot = column inside the wave (0..kCW-1).
 static_assert(4 * kCW <= 255, "slot index must fit the 8-bit gpr_idx field");
 static_assert(64 * 16 <= 1024, "lane byte offset (16*lane) must fit the 10 low address bits");
@@ -54,6 +65,7 @@ struct PlanOut {
 
 struct GemmArgs {
     const float* X = nullptr;
+    float* XT = nullptr;       // K x ldxt workspace: X transposed (ldxt = M rounded up to kTM)
     int M = 0, K = 0;
     const int2* ent = nullptr;
     const int* sptr = nullptr;
@@ -78,6 +90,7 @@ hipError_t plan_fill(const PlanDev& in, PlanOut& out, hipStream_t st);      // -
 // Launch
 int choose_slices(int M, int ncols, int K, long long nnz, int n_groups, size_t ws_bytes, int force);
 size_t workspace_bytes(int M, int ncols, int slices);
+size_t xt_bytes(int M, int K);
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st);
 // tcsc_from_dense on the device
 hipError_t dense_to_tcsc_counts(const float* D, int rows, int cols, int* cntp, int* cntn, hipStream_t st);

@@ -34,6 +34,8 @@
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "tcsc_internal.h"
 
 namespace tcsc {
@@ -89,7 +91,7 @@ __global__ void k_group_counts(const int* __restrict__ cptr, int ncols, int nch,
     }
 }
 
-__device__ __forceinline__ int lds_row_of(int c, int k_local) { return (c & 1) * kBufRows + k_local; }
+__device__ __forceinline__ int lds_row_of(int c, int k_local) { return (c % kNBuf) * kBufRows + k_local; }
 
 // Scatter the +1 (SIGN=0) or -1 (SIGN=1) entries to their stream slot.
 // Inside a (chunk, group) stream the columns follow each other and every
@@ -145,93 +147,77 @@ __global__ void k_fill_pads(const int* __restrict__ cptr, const int* __restrict_
 // K1: the gather kernel
 // ---------------------------------------------------------------------------
 
-// Transposed staging of X[m0..m0+255][k0..k0+63] into an LDS buffer laid out
-// [k][256 rows].  Each thread owns two 4x4 blocks (4 rows x 4 k): four
-// coalesced float4 loads (rows), a register transpose, four ds_write_b128
-// (k rows).  Lanes 0-7 of a wave own consecutive row quads so every 8-lane
-// write group stores 128 contiguous bytes (conflict-free), and per load
-// instruction the wave reads 8 rows x 128 B.
-struct Stage {
-    float4 v[2][4];
-};
-
-// Branch-free and select-free loads, so all eight issue back to back and are
-// waited for once, at stage_store.  Values staged for rows >= M or k >= K are
-// never used (no stream entry points at a k row past K, and rows past M are
-// not stored), so only memory safety matters: VEC4 (K % 4 == 0, X 16-B
-// aligned, (M+256)*K*4 < 2^31) uses raw buffer loads, whose range check
-// returns 0 past the end of X; one 32-bit offset VGPR per row keeps address
-// registers few, so the staged tile stays out of the registers the gather
-// asm owns.  Otherwise clamped scalar loads.
-template <bool VEC4>
-__device__ __forceinline__ void stage_load(Stage& s, const float* __restrict__ X, int M, int K, int m0, int k0) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int mq = (lane & 7) + 8 * w;  // 0..63
-    if (VEC4) {
-        const __amdgpu_buffer_rsrc_t rsrc =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X), (short)0, M * K * 4, 0x00020000);
+// X (M x K, row-major) -> XT (K x ldxt), ldxt = M rounded up to kTM; the
+// rows m in [M, ldxt) are written as 0.  64x64 tiles through LDS (the +1
+// column makes both the row writes and the column reads conflict-free);
+// HBM-bound: 2*M*K*4 bytes per call.
+__global__ void __launch_bounds__(256) k_transpose(const float* __restrict__ X, int M, int K, float* __restrict__ XT,
+                                                   int ldxt) {
+    __shared__ float t[64][65];
+    const int k0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int kk = k0 + 4 * ((lane >> 3) + 8 * h);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const unsigned off = (unsigned)((m0 + 4 * mq + r) * K + kk) * 4u;
-                s.v[h][r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
-            }
-        }
-        return;
+    for (int i = 0; i < 16; ++i) {
+        const int r = ty + 4 * i, m = m0 + r, k = k0 + tx;
+        t[r][tx] = (m < M && k < K) ? X[(size_t)m * K + k] : 0.f;
     }
+    __syncthreads();
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int kk = k0 + 4 * ((lane >> 3) + 8 * h);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = min(m0 + 4 * mq + r, M - 1);
-            const float* src = X + (size_t)row * K;
-            s.v[h][r] = make_float4(src[min(kk, K - 1)], src[min(kk + 1, K - 1)], src[min(kk + 2, K - 1)],
-                                    src[min(kk + 3, K - 1)]);
-        }
-    }
-}
-
-__device__ __forceinline__ void stage_store(const Stage& s, char* __restrict__ buf) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int mq = (lane & 7) + 8 * w;
-        const int kq = (lane >> 3) + 8 * h;
-        char* p = buf + (4 * kq) * kRowBytes + mq * 16;
-        *reinterpret_cast<float4*>(p + 0 * kRowBytes) = make_float4(s.v[h][0].x, s.v[h][1].x, s.v[h][2].x, s.v[h][3].x);
-        *reinterpret_cast<float4*>(p + 1 * kRowBytes) = make_float4(s.v[h][0].y, s.v[h][1].y, s.v[h][2].y, s.v[h][3].y);
-        *reinterpret_cast<float4*>(p + 2 * kRowBytes) = make_float4(s.v[h][0].z, s.v[h][1].z, s.v[h][2].z, s.v[h][3].z);
-        *reinterpret_cast<float4*>(p + 3 * kRowBytes) = make_float4(s.v[h][0].w, s.v[h][1].w, s.v[h][2].w, s.v[h][3].w);
+    for (int i = 0; i < 16; ++i) {
+        const int kk = ty + 4 * i, k = k0 + kk;
+        if (k < K) XT[(size_t)k * ldxt + m0 + tx] = t[tx][kk];
     }
 }
 
 #include "gather_asm.inc"
 
 // Consume this wave's stream for one chunk: `nb` batches of 8 entries at
-// `stream` (entries padded to a multiple of 8; the first 64-entry block is
-// already in e_sgn/e_w1, lane i = entry i).  The schedule and register map
-// are in tools/gen_gather_asm.py.  M0 is written by s_set_gpr_idx_*; it is a
-// reserved register the compiler keeps nothing in for this kernel (no
-// LDS-DMA, movrel or message instructions).
-__device__ __forceinline__ void gather_stream(const int2* __restrict__ stream, unsigned nb, int e_sgn, int e_w1,
-                                              unsigned lane_off, unsigned mask, f32x32& a0, f32x32& a1,
-                                              f32x32& a2, f32x32& a3) {
-    unsigned voff = (lane_off >> 4) * 8u;  // byte offset of this lane's entry in a block
-    asm volatile(TCSC_GATHER_ASM
+// `stream` (entries padded to a multiple of 8).  The chunk's first 64-entry
+// block (lane i = entry i) is already in the PAR pair (v232/v233 for even
+// chunks, v238/v239 for odd ones); the asm starts by loading the next
+// chunk's first block (at `next`) into the other pair, so that load has a
+// whole chunk to land.  The schedule and register map are in
+// tools/gen_gather_asm.py.  s_set_gpr_idx_* writes M0, which the compiler
+// also uses (LDS-DMA destination): the asm saves it in s68 and restores it.
+#define TCSC_GATHER_CLOBBERS                                                                                        \
+    "memory", "scc", "v168", "v169", "v170", "v171", "v172", "v173", "v174", "v175", "v176", "v177", "v178", "v179",  \
+        "v180", "v181", "v182", "v183", "v184", "v185", "v186", "v187", "v188", "v189", "v190", "v191", "v192",       \
+        "v193", "v194", "v195", "v196", "v197", "v198", "v199", "v200", "v201", "v202", "v203", "v204", "v205",       \
+        "v206", "v207", "v208", "v209", "v210", "v211", "v212", "v213", "v214", "v215", "v216", "v217", "v218",       \
+        "v219", "v220", "v221", "v222", "v223", "v224", "v225", "v226", "v227", "v228", "v229", "v230", "v231",       \
+        "v234", "v235", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48",     \
+        "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63",       \
+        "s64", "s65", "s66", "s67", "s68"
+
+struct EntryRegs {
+    int s0, w0;  // pinned to v232/v233
+    int s1, w1;  // pinned to v238/v239
+};
+
+template <int PAR>
+__device__ __forceinline__ void gather_stream(const int2* __restrict__ stream, const int2* __restrict__ next,
+                                              unsigned nb, EntryRegs& er, unsigned lane, unsigned mask, f32x32& a0,
+                                              f32x32& a1, f32x32& a2, f32x32& a3) {
+    unsigned voff = lane * 8u;  // byte offset of this lane's entry in a block
+    asm volatile(TCSC_GATHER_ASM_0
                  : [nb] "+s"(nb), "+{v[40:71]}"(a0), "+{v[72:103]}"(a1), "+{v[104:135]}"(a2),
-                   "+{v[136:167]}"(a3), "+{v232}"(e_sgn), "+{v233}"(e_w1), "+{v236}"(voff)
-                 : [ent] "s"(stream), [lane] "v"(lane_off), [mask] "v"(mask)
-                 : "memory", "scc", "v168", "v169", "v170", "v171", "v172", "v173", "v174", "v175", "v176",
-                   "v177", "v178", "v179", "v180", "v181", "v182", "v183", "v184", "v185", "v186", "v187", "v188",
-                   "v189", "v190", "v191", "v192", "v193", "v194", "v195", "v196", "v197", "v198", "v199", "v200",
-                   "v201", "v202", "v203", "v204", "v205", "v206", "v207", "v208", "v209", "v210", "v211", "v212",
-                   "v213", "v214", "v215", "v216", "v217", "v218", "v219", "v220", "v221", "v222", "v223", "v224",
-                   "v225", "v226", "v227", "v228", "v229", "v230", "v231", "v234", "v235", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43",
-                   "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57",
-                   "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67");
+                   "+{v[136:167]}"(a3), "+{v232}"(er.s0), "+{v233}"(er.w0), "+{v238}"(er.s1), "+{v239}"(er.w1),
+                   "+{v236}"(voff)
+                 : [ent] "s"(stream), [nent] "s"(next), [lane] "v"(lane * 16u), [mask] "v"(mask)
+                 : TCSC_GATHER_CLOBBERS);
+}
+
+template <>
+__device__ __forceinline__ void gather_stream<1>(const int2* __restrict__ stream, const int2* __restrict__ next,
+                                                 unsigned nb, EntryRegs& er, unsigned lane, unsigned mask,
+                                                 f32x32& a0, f32x32& a1, f32x32& a2, f32x32& a3) {
+    unsigned voff = lane * 8u;
+    asm volatile(TCSC_GATHER_ASM_1
+                 : [nb] "+s"(nb), "+{v[40:71]}"(a0), "+{v[72:103]}"(a1), "+{v[104:135]}"(a2),
+                   "+{v[136:167]}"(a3), "+{v232}"(er.s0), "+{v233}"(er.w0), "+{v238}"(er.s1), "+{v239}"(er.w1),
+                   "+{v236}"(voff)
+                 : [ent] "s"(stream), [nent] "s"(next), [lane] "v"(lane * 16u), [mask] "v"(mask)
+                 : TCSC_GATHER_CLOBBERS);
 }
 
 // i is a compile-time constant after unrolling
@@ -246,12 +232,31 @@ __device__ __forceinline__ void acc_set(f32x32& a0, f32x32& a1, f32x32& a2, f32x
     else a3[i - 96] = v;
 }
 
+// Issue this wave's LDS-DMA rows of chunk c (clamped to the last chunk, so
+// the look-ahead past the end stays branch-free) into ring buffer `buf`:
+// row k of the chunk = XT[k][m0..m0+255], one 1-KiB global_load_lds_dwordx4
+// per row (lane l moves rows m0+4l..4l+3).  kDmaPerWave VMEM ops per wave.
+__device__ __forceinline__ void dma_chunk(char* lds, const float* __restrict__ xcol, size_t ldxt, int K, int nch,
+                                          int c, int buf, int wave) {
+#if (defined(TCSC_ABLATION) && TCSC_ABLATION == 6) || defined(TCSC_NODMA)
+    return;  // timing only: no staging
+#endif
+    const int cc = min(c, nch - 1);
+    char* dst = lds + buf * (kBufRows * kRowBytes);
+#pragma unroll
+    for (int i = 0; i < kDmaPerWave; ++i) {
+        const int kl = wave * kDmaPerWave + i;
+        const int k = min(cc * kTK + kl, K - 1);
+        __builtin_amdgcn_global_load_lds(xcol + (size_t)k * ldxt, dst + kl * kRowBytes, 16, 0, 0);
+    }
+}
+
 // OUT: 0 = final Y (bias + activation), 1 = partial slab ws[slice][M][ncols]
-template <bool BIAS_FIRST, bool PRELU, bool VEC4, int OUT>
+template <bool BIAS_FIRST, bool PRELU, int OUT>
 __global__ void __launch_bounds__(kWaves * 64, 2)
-k_stream(const float* __restrict__ X, int M, int K, const int2* __restrict__ ent, const int* __restrict__ sptr,
-         int G, int ncols, int nch, int chunks_per_slice, const float* __restrict__ Bias, float* __restrict__ Y,
-         int ldy, float a, float* __restrict__ ws) {
+k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __restrict__ ent,
+         const int* __restrict__ sptr, int G, int ncols, int nch, int chunks_per_slice, const float* __restrict__ Bias,
+         float* __restrict__ Y, int ldy, float a, float* __restrict__ ws) {
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -282,84 +287,155 @@ k_stream(const float* __restrict__ X, int M, int K, const int2* __restrict__ ent
         }
     }
 
-    // the -0.0 pad rows of both buffers (entries padding a stream point here)
-    if (threadIdx.x < 64) {
-        reinterpret_cast<float4*>(lds + kTK * kRowBytes)[threadIdx.x] = make_float4(-0.f, -0.f, -0.f, -0.f);
-        reinterpret_cast<float4*>(lds + (kBufRows + kTK) * kRowBytes)[threadIdx.x] =
-            make_float4(-0.f, -0.f, -0.f, -0.f);
+    // the -0.0 pad row of every ring buffer (entries padding a stream point here)
+    if (threadIdx.x < 64 * kNBuf) {
+        const int b = threadIdx.x >> 6;
+        reinterpret_cast<float4*>(lds + (b * kBufRows + kTK) * kRowBytes)[lane] = make_float4(-0.f, -0.f, -0.f, -0.f);
     }
-    Stage st;
-    if (c_begin < c_end) {
-        stage_load<VEC4>(st, X, M, K, m0, c_begin * kTK);
-        stage_store(st, lds + (c_begin & 1) * kBufRows * kRowBytes);
-    }
-    __syncthreads();
 
-    const unsigned lane_off = 16u * lane;
-    const unsigned mask = 0x3ffu;
-    // Software-pipelined chunk loop.  Stream bounds come 64 chunks at a time
-    // (lane i = chunk cb+i) and are read with readlane; the first entry block
-    // of chunk c+1 is loaded during chunk c, before the staging loads, so the
-    // gather's input was issued a whole chunk earlier.  No branches around
-    // the loads: staging the chunk after the last one and streams of idle
-    // waves are harmless (clamped reads, nb = 0, an LDS buffer nobody reads).
-    const int gi = active ? g : G - 1;
-    int cb = c_begin;
-    int vs0 = 0, vs1 = 0;
-    int2 en = make_int2(0, 0);
-    int s0n = 0, s1n = 0;
     if (c_begin < c_end) {
-        const long long ci = (long long)min(cb + lane, nch - 1) * G + gi;
-        vs0 = sptr[ci];
-        vs1 = sptr[ci + 1];
-        s0n = __builtin_amdgcn_readlane(vs0, 0);
-        s1n = __builtin_amdgcn_readlane(vs1, 0);
-        en = ent[s0n + lane];
-    }
-    for (int c = c_begin; c < c_end; ++c) {
-        const int s0 = s0n, s1 = s1n;
-        const int2 e = en;
-        int idx = c + 1 - cb;
-        if (idx == 64) {
-            cb += 64;
-            idx = 0;
-            const long long ci = (long long)min(cb + lane, nch - 1) * G + gi;
-            vs0 = sptr[ci];
-            vs1 = sptr[ci + 1];
+        // Chunk c lives in ring buffer c % 3 (the plan baked that into every
+        // entry); DMA(c+2) is issued right after gather(c), so two chunks are
+        // in flight while one is consumed.  Per wave the VMEM order is
+        //   ... DMA(c) | E(c) [+ block loads, waited inside] | DMA(c+1) | E(c+1) ...
+        // (E = the chunk's first entry block, loaded by gather(c-1)), so at
+        // the top of chunk c, vmcnt(kDmaPerWave) means DMA(c) and E(c) have
+        // landed; the barrier then makes every wave's rows of chunk c
+        // visible and says all waves are done reading chunk c-1's buffer,
+        // which DMA(c+2) reuses.  All loads in the loop are asm or LDS-DMA,
+        // so the compiler inserts no waits of its own.
+        const float* xcol = XT + m0 + 4 * lane;
+        const size_t ld = (size_t)ldxt;
+        int buf = c_begin % kNBuf;
+        dma_chunk(lds, xcol, ld, K, nch, c_begin, buf, wave);
+
+        const int gi = active ? g : G - 1;
+        int cb = c_begin;
+        long long ci = (long long)min(cb + lane, nch - 1) * G + gi;
+        int vs0 = sptr[ci], vs1 = sptr[ci + 1];
+        int s0n = __builtin_amdgcn_readfirstlane(vs0);
+        int s1n = __builtin_amdgcn_readfirstlane(vs1);
+        EntryRegs er;
+        asm volatile("global_load_dwordx2 v[232:233], %2, %3"
+                     : "={v232}"(er.s0), "={v233}"(er.w0)
+                     : "v"(lane * 8u), "s"(ent + s0n)
+                     : "memory");
+        er.s1 = 0;
+        er.w1 = 0;
+        dma_chunk(lds, xcol, ld, K, nch, c_begin + 1, buf == kNBuf - 1 ? 0 : buf + 1, wave);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // pad rows
+
+        const unsigned mask = 0x3ffu;
+        auto chunk = [&](int c, bool valid, auto par) {
+            constexpr int PAR = decltype(par)::value;
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDmaPerWave) : "memory");
+            __builtin_amdgcn_s_barrier();
+            const int s0 = s0n, s1 = s1n;
+            const int idx = c + 1 - cb;
+            if (idx == 64) {  // next 64 chunks' stream bounds
+                cb += 64;
+                ci = (long long)min(cb + lane, nch - 1) * G + gi;
+                vs0 = sptr[ci];
+                vs1 = sptr[ci + 1];
+                s0n = __builtin_amdgcn_readfirstlane(vs0);
+                s1n = __builtin_amdgcn_readfirstlane(vs1);
+            } else {
+                s0n = __builtin_amdgcn_readlane(vs0, idx);
+                s1n = __builtin_amdgcn_readlane(vs1, idx);
+            }
+            const unsigned nb = (active && valid) ? (unsigned)(s1 - s0) / kBatch : 0u;
+            gather_stream<PAR>(ent + s0, ent + s0n, nb, er, lane, mask, a0, a1, a2, a3);
+            int b2 = buf + 2;
+            if (b2 >= kNBuf) b2 -= kNBuf;
+            dma_chunk(lds, xcol, ld, K, nch, c + 2, b2, wave);
+            buf = buf == kNBuf - 1 ? 0 : buf + 1;
+        };
+        // unrolled by 2 for the entry-block parity; an odd chunk count runs
+        // one empty step (nb = 0; its DMA and look-ahead are clamped)
+        for (int c = c_begin; c < c_end; c += 2) {
+            chunk(c, true, std::integral_constant<int, 0>());
+            chunk(c + 1, c + 1 < c_end, std::integral_constant<int, 1>());
         }
-        s0n = __builtin_amdgcn_readlane(vs0, idx);
-        s1n = __builtin_amdgcn_readlane(vs1, idx);
-        en = ent[s0n + lane];
-        asm volatile("" ::: "memory");  // keep the entry load ahead of the staging loads
-        stage_load<VEC4>(st, X, M, K, m0, (c + 1) * kTK);
-        const unsigned nb = active ? (unsigned)(s1 - s0) / kBatch : 0u;
-        gather_stream(ent + s0, nb, e.x, e.y, lane_off, mask, a0, a1, a2, a3);
-        stage_store(st, lds + ((c + 1) & 1) * kBufRows * kRowBytes);
-        __syncthreads();
+        // no LDS-DMA may still be writing when the workgroup's LDS is released
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 
-    if (!active) return;
+    // Epilogue: lanes hold rows (4 per lane), so a direct store would put
+    // 64 rows' 4-byte pieces in one instruction (partial-line writes that
+    // cost ~16x the bytes in HBM writes).  Transpose through LDS instead:
+    // per half tile (128 rows) every wave parks its 128 x 32 block (16 KiB,
+    // row stride 128 B, 16-B quads XOR-swizzled by row/4 so the b128
+    // writes and reads spread over the banks), then reads it back as rows:
+    // 8 lanes per 128-B row segment, 16-B stores.
+    __syncthreads();  // every wave is done with the tile ring
+    char* region = lds + wave * (128 * 128);
+    const int lh = lane & 31;
+    const int col0 = g * kCW;
+    const bool vec_ok = OUT == 0 ? ((ldy & 3) == 0 && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0))
+                                 : ((ncols & 3) == 0 && ((reinterpret_cast<uintptr_t>(ws) & 15) == 0));
 #pragma unroll
-    for (int j = 0; j < kCW; ++j) {
-        const int col = g * kCW + j;
-        if (col < ncols) {
-            float b = 0.f;
-            if (OUT == 0 && !BIAS_FIRST) b = Bias[col];
+    for (int h = 0; h < 2; ++h) {
+        if (active && (lane >> 5) == h) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = m0 + 4 * lane + r;
-                if (row < M) {
-                    float v = acc_get(a0, a1, a2, a3, 4 * j + r);
+                const int R = 4 * lh + r;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const float4 v = make_float4(acc_get(a0, a1, a2, a3, 4 * (4 * q + 0) + r),
+                                                 acc_get(a0, a1, a2, a3, 4 * (4 * q + 1) + r),
+                                                 acc_get(a0, a1, a2, a3, 4 * (4 * q + 2) + r),
+                                                 acc_get(a0, a1, a2, a3, 4 * (4 * q + 3) + r));
+                    *reinterpret_cast<float4*>(region + R * 128 + ((q ^ (lh & 7)) << 4)) = v;
+                }
+            }
+        }
+        __syncthreads();
+        if (active) {
+            const int q = lane & 7;
+            const int col = col0 + 4 * q;
+            float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (OUT == 0 && !BIAS_FIRST) {
+                bq.x = col + 0 < ncols ? Bias[col + 0] : 0.f;
+                bq.y = col + 1 < ncols ? Bias[col + 1] : 0.f;
+                bq.z = col + 2 < ncols ? Bias[col + 2] : 0.f;
+                bq.w = col + 3 < ncols ? Bias[col + 3] : 0.f;
+            }
+#pragma unroll 4
+            for (int i = 0; i < 16; ++i) {
+                const int R = (lane >> 3) + 8 * i;
+                const int row = m0 + 128 * h + R;
+                float4 v = *reinterpret_cast<const float4*>(region + R * 128 + ((q ^ ((R >> 2) & 7)) << 4));
+                if (row < M && col < ncols) {
+                    float* dst;
                     if (OUT == 0) {
-                        if (!BIAS_FIRST) v += b;
-                        if (PRELU) v = (v < 0.0f) ? a * v : v;
-                        Y[(size_t)row * ldy + col] = v;
+                        if (!BIAS_FIRST) {
+                            v.x += bq.x;
+                            v.y += bq.y;
+                            v.z += bq.z;
+                            v.w += bq.w;
+                        }
+                        if (PRELU) {
+                            v.x = (v.x < 0.0f) ? a * v.x : v.x;
+                            v.y = (v.y < 0.0f) ? a * v.y : v.y;
+                            v.z = (v.z < 0.0f) ? a * v.z : v.z;
+                            v.w = (v.w < 0.0f) ? a * v.w : v.w;
+                        }
+                        dst = Y + (size_t)row * ldy + col;
                     } else {
-                        ws[((size_t)blockIdx.z * M + row) * ncols + col] = v;
+                        dst = ws + ((size_t)blockIdx.z * M + row) * ncols + col;
+                    }
+                    if (vec_ok && col + 3 < ncols) {
+                        *reinterpret_cast<float4*>(dst) = v;
+                    } else {
+                        dst[0] = v.x;
+                        if (col + 1 < ncols) dst[1] = v.y;
+                        if (col + 2 < ncols) dst[2] = v.z;
+                        if (col + 3 < ncols) dst[3] = v.w;
                     }
                 }
             }
         }
+        if (h == 0) __syncthreads();  // region reused by the second half
     }
 }
 
@@ -473,10 +549,18 @@ size_t workspace_bytes(int M, int ncols, int slices) {
     return slices > 1 ? (size_t)slices * M * ncols * sizeof(float) : 0;
 }
 
+static inline int ldxt_of(int M) { return (M + kTM - 1) / kTM * kTM; }
+
+// X^T of one call: K x ldxt floats, 256-B aligned size.
+size_t xt_bytes(int M, int K) {
+    const size_t b = (size_t)K * ldxt_of(M) * sizeof(float);
+    return (b + 255) / 256 * 256;
+}
+
 // Cost model (cycles of one CU at ~2.1 GHz) for k-slicing: every workgroup
 // runs on its own CU; gathers cost ~1 KiB / 220 B/clk per nonzero and
-// wave, staging ~1 KiB / 79 B/clk per k row (MI355X_MICROARCH.md LDS rows,
-// DESIGN.md measurements); the split-K slabs cost HBM time.
+// wave, the LDS-DMA ~1 KiB / 100 B/clk per k row (DESIGN.md
+// measurements); the split-K slabs cost HBM time.
 int choose_slices(int M, int ncols, int K, long long nnz, int G, size_t ws_bytes, int force) {
     const int nch = (K + kTK - 1) / kTK;
     if (nch <= 1) return 1;
@@ -486,7 +570,7 @@ int choose_slices(int M, int ncols, int K, long long nnz, int G, size_t ws_bytes
     auto cap = [&](int s) { return s <= nch && workspace_bytes(M, ncols, s) <= ws_bytes; };
     if (force > 0) return cap(force) ? force : 1;
     const double nz_per_chunk_block = (double)nnz / nch / cb;  // per workgroup and chunk (all its waves)
-    const double chunk_cycles = nz_per_chunk_block * (1024.0 / 220.0) + kTK * (1024.0 / 79.0) + 600.0;
+    const double chunk_cycles = nz_per_chunk_block * (1024.0 / 220.0) + kTK * (1024.0 / 100.0) + 400.0;
     double best = 1e300;
     int best_s = 1;
     for (int s = 1; s <= 16; ++s) {
@@ -505,27 +589,20 @@ int choose_slices(int M, int ncols, int K, long long nnz, int G, size_t ws_bytes
 }
 
 template <bool BF, bool PR>
-static hipError_t launch_t(const GemmArgs& g, int slices, bool vec4, hipStream_t st) {
+static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
     const int nch = (g.K + kTK - 1) / kTK;
     int cps = nch > 0 ? (nch + slices - 1) / slices : 1;
     slices = nch > 0 ? (nch + cps - 1) / cps : 1;
+    const int ldxt = ldxt_of(g.M);
     dim3 grid((g.n_groups + kWaves - 1) / kWaves, (g.M + kTM - 1) / kTM, slices);
     dim3 block(kWaves * 64);
     if (slices == 1) {
-        if (vec4)
-            hipLaunchKernelGGL((k_stream<BF, PR, true, 0>), grid, block, 0, st, g.X, g.M, g.K, g.ent, g.sptr,
-                               g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
-        else
-            hipLaunchKernelGGL((k_stream<BF, PR, false, 0>), grid, block, 0, st, g.X, g.M, g.K, g.ent, g.sptr,
-                               g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
+        hipLaunchKernelGGL((k_stream<BF, PR, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
+                           g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
         return hipGetLastError();
     }
-    if (vec4)
-        hipLaunchKernelGGL((k_stream<BF, PR, true, 1>), grid, block, 0, st, g.X, g.M, g.K, g.ent, g.sptr, g.n_groups,
-                           g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
-    else
-        hipLaunchKernelGGL((k_stream<BF, PR, false, 1>), grid, block, 0, st, g.X, g.M, g.K, g.ent, g.sptr,
-                           g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
+    hipLaunchKernelGGL((k_stream<BF, PR, 1>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr, g.n_groups,
+                       g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const long long total = (long long)g.M * g.ncols;
@@ -534,15 +611,21 @@ static hipError_t launch_t(const GemmArgs& g, int slices, bool vec4, hipStream_t
     return hipGetLastError();
 }
 
+// g.XT must hold xt_bytes(M, K) (the API layer carves it out of the plan's
+// workspace, ahead of the split-K slabs in g.ws).
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
     if (g.M <= 0 || g.ncols <= 0) return hipSuccess;
-    const bool vec4 = (g.K % 4 == 0) && ((reinterpret_cast<uintptr_t>(g.X) & 15) == 0) &&
-                      ((long long)(g.M + kTM) * g.K * 4 < (1LL << 31));
-    const int s = choose_slices(g.M, g.ncols, g.K, g.nnz, g.n_groups, g.ws ? g.ws_bytes : 0, g.force_slices);
-    if (g.bias_first) {
-        return g.prelu ? launch_t<true, true>(g, s, vec4, st) : launch_t<true, false>(g, s, vec4, st);
+    if (g.K > 0) {
+        if (!g.XT) return hipErrorInvalidValue;
+        const int ldxt = ldxt_of(g.M);
+        hipLaunchKernelGGL(k_transpose, dim3((g.K + 63) / 64, ldxt / 64), dim3(256), 0, st, g.X, g.M, g.K, g.XT,
+                           ldxt);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
     }
-    return g.prelu ? launch_t<false, true>(g, s, vec4, st) : launch_t<false, false>(g, s, vec4, st);
+    const int s = choose_slices(g.M, g.ncols, g.K, g.nnz, g.n_groups, g.ws ? g.ws_bytes : 0, g.force_slices);
+    if (g.bias_first) return g.prelu ? launch_t<true, true>(g, s, st) : launch_t<true, false>(g, s, st);
+    return g.prelu ? launch_t<false, true>(g, s, st) : launch_t<false, false>(g, s, st);
 }
 
 hipError_t dense_to_tcsc_counts(const float* D, int rows, int cols, int* cntp, int* cntn, hipStream_t st) {

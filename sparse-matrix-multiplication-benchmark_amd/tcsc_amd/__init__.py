@@ -20,7 +20,9 @@ import subprocess
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libtcsc_amd.so")
+# TCSC_AMD_LIB points at an alternative build (e.g. the timing-only ablation
+# builds of `make ablation`); default: the in-tree library.
+LIB_PATH = os.environ.get("TCSC_AMD_LIB") or os.path.join(PKG_DIR, "lib", "libtcsc_amd.so")
 
 VARIANTS = ("basic", "optimized", "prelu_basic", "prelu_separate", "prelu_onthego")
 VARIANT_ID = {v: i for i, v in enumerate(VARIANTS)}

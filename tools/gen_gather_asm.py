@@ -22,15 +22,25 @@ and returns out of order); the next block is prefetched at each block start.
 
 Registers: acc v40..v167 (pinned asm operands), X v168..v231 (each LDS
 address is computed into the first register of its destination quad),
-entry blocks v232..v235, block offset v236; SGPR sets s36..s67.
+entry blocks v232..v235, block offset v236; SGPR sets s36..s67; s68 holds
+the caller's M0 (s_set_gpr_idx_* overwrites it) and is restored on exit.
 """
 import os
 import sys
 
 SETS = {0: 36, 1: 52}          # SGPR set base: pair i = (s[base+2i] sign, s[base+2i+1] word1)
 XSET = {0: 168, 1: 200}        # X set base: entry i -> v[base+4i : base+4i+3]
-EBLK = {0: (232, 233), 1: (234, 235)}  # entry block VGPRs (sign, word1)
+# entry block VGPRs (sign, word1): block A is the chunk's first block, which
+# the previous chunk's gather prefetched; it alternates between v232/v233 and
+# v238/v239 with the chunk parity (PAR), the other pair receives the next
+# chunk's first block.  Block B is internal.
+EBLK_A = {0: (232, 233), 1: (238, 239)}  # VGPR tuples must be even-aligned
+EBLK = {0: EBLK_A[0], 1: (234, 235)}
 VOFF = "v236"
+PAR = 0
+
+
+ABL = 0  # ablation (timing experiments only; results are wrong for ABL != 0)
 
 
 def issue(p):
@@ -41,14 +51,21 @@ def issue(p):
     lane0 = 8 * (p % 8)
     out = []
     for i in range(8):
-        out.append(f"v_readlane_b32 s{s + 2 * i + 1}, v{vw1}, {lane0 + i}")
+        if ABL == 2:
+            out.append(f"s_mov_b32 s{s + 2 * i + 1}, {4 * i}")
+        else:
+            out.append(f"v_readlane_b32 s{s + 2 * i + 1}, v{vw1}, {lane0 + i}")
     for i in range(8):
-        out.append(f"v_readlane_b32 s{s + 2 * i}, v{vsgn}, {lane0 + i}")
+        if ABL == 2:
+            out.append(f"s_mov_b32 s{s + 2 * i}, 1.0")
+        else:
+            out.append(f"v_readlane_b32 s{s + 2 * i}, v{vsgn}, {lane0 + i}")
     # the address goes into the first register of the destination quad
     for i in range(8):
         out.append(f"v_bfi_b32 v{x + 4 * i}, %[mask], %[lane], s{s + 2 * i + 1}")
     for i in range(8):
-        out.append(f"ds_read_b128 v[{x + 4 * i}:{x + 4 * i + 3}], v{x + 4 * i}")
+        if ABL != 3:
+            out.append(f"ds_read_b128 v[{x + 4 * i}:{x + 4 * i + 3}], v{x + 4 * i}")
     return out
 
 
@@ -56,13 +73,18 @@ def fma(parity, wait):
     s = SETS[parity]
     x = XSET[parity]
     out = [f"s_waitcnt lgkmcnt({wait})"]
+    if ABL == 4:
+        return out
     for i in range(8):
         w1 = f"s{s + 2 * i + 1}"
         pair = f"s[{s + 2 * i}:{s + 2 * i + 1}]"
-        out.append(f"s_set_gpr_idx_on {w1}, gpr_idx(SRC2,DST)" if i == 0 else f"s_set_gpr_idx_idx {w1}")
-        out.append(f"v_pk_fma_f32 v[40:41], v[{x + 4 * i}:{x + 4 * i + 1}], {pair}, v[40:41] op_sel_hi:[1,0,1]")
-        out.append(f"v_pk_fma_f32 v[42:43], v[{x + 4 * i + 2}:{x + 4 * i + 3}], {pair}, v[42:43] op_sel_hi:[1,0,1]")
-    out.append("s_set_gpr_idx_off")
+        a = 40 + 4 * i if ABL == 1 else 40
+        if ABL != 1:
+            out.append(f"s_set_gpr_idx_on {w1}, gpr_idx(SRC2,DST)" if i == 0 else f"s_set_gpr_idx_idx {w1}")
+        out.append(f"v_pk_fma_f32 v[{a}:{a + 1}], v[{x + 4 * i}:{x + 4 * i + 1}], {pair}, v[{a}:{a + 1}] op_sel_hi:[1,0,1]")
+        out.append(f"v_pk_fma_f32 v[{a + 2}:{a + 3}], v[{x + 4 * i + 2}:{x + 4 * i + 3}], {pair}, v[{a + 2}:{a + 3}] op_sel_hi:[1,0,1]")
+    if ABL != 1:
+        out.append("s_set_gpr_idx_off")
     return out
 
 
@@ -89,7 +111,10 @@ def step_end(p):
 
 
 def generate():
-    L = []
+    na = EBLK_A[1 - PAR]
+    L = ["s_mov_b32 s68, m0"]  # M0 also addresses the caller's LDS-DMA
+    # next chunk's first entry block (VOFF = lane*8 on entry)
+    L.append(f"global_load_dwordx2 v[{na[0]}:{na[1]}], {VOFF}, %[nent]")
     L.append("s_cmp_eq_u32 %[nb], 0")
     L.append("s_cbranch_scc1 .Lend%=")
     # prologue: block A is the caller-provided input; maybe prefetch block B
@@ -114,21 +139,38 @@ def generate():
         if par == 0:
             L.append("s_branch .Lend%=")
     L.append(".Lend%=:")
+    L.append("s_mov_b32 m0, s68")
     return L
 
 
+def emit(f, lines):
+    f.write(f"#define TCSC_GATHER_ASM_{PAR} \\\n")
+    for l in lines:
+        f.write(f'    "{l}\\n\\t" \\\n')
+    f.write('    ""\n')
+
+
 def main():
+    global ABL, PAR, EBLK
     here = os.path.dirname(os.path.abspath(__file__))
     out = os.path.join(here, "..", "sparse-matrix-multiplication-benchmark_amd", "csrc", "gather_asm.inc")
-    lines = generate()
     with open(out, "w") as f:
         f.write("// GENERATED by tools/gen_gather_asm.py -- do not edit by hand.\n")
-        f.write(f"// {len(lines)} lines; see the generator's docstring for the schedule.\n")
-        f.write("#define TCSC_GATHER_ASM \\\n")
-        for l in lines:
-            f.write(f'    "{l}\\n\\t" \\\n')
-        f.write('    ""\n')
-    print(out, len(lines), "lines")
+        f.write("// See the generator's docstring for the schedule.  TCSC_ABLATION != 0\n")
+        f.write("// selects timing-only variants (wrong results) for experiments.\n")
+        f.write("#if !defined(TCSC_ABLATION) || TCSC_ABLATION == 0 || TCSC_ABLATION >= 6\n")
+        for a in (0, 1, 2, 3, 4, 5):
+            if a:
+                f.write(f"#elif TCSC_ABLATION == {a}\n")
+            ABL = a
+            for PAR in (0, 1):
+                EBLK = {0: EBLK_A[PAR], 1: (234, 235)}
+                if a == 5:  # no gather at all: only the M0 save and next-block load
+                    emit(f, generate()[:2] + ["s_mov_b32 m0, s68"])
+                else:
+                    emit(f, generate())
+        f.write("#endif\n")
+    print(out)
 
 
 if __name__ == "__main__":
