@@ -81,10 +81,14 @@ int tcsc_gpu_plan_create_device(int rows, int cols,
 
 int tcsc_gpu_plan_get_info(const tcsc_gpu_plan *plan, tcsc_gpu_plan_info *info);
 
-/* Allocate the plan's split-K workspace for launches of up to `max_M` rows
- * (small grids split K over workgroups and combine fp32 partial slabs in a
- * fixed order).  Optional: without it tcsc_gpu_sgemm never splits.  Not
- * thread-safe against concurrent launches of the same plan. */
+/* Allocate the plan's workspace for launches of up to `max_M` rows: X^T
+ * (K x max_M rounded up to 256 floats; the kernel streams X^T rows into LDS)
+ * plus, where the cost model splits K over workgroups, the fp32 partial
+ * slabs combined in a fixed order.  Optional: tcsc_gpu_sgemm grows the
+ * workspace itself on the first call with a larger M (that call then
+ * allocates and synchronises the device); reserving up front keeps every
+ * sgemm call allocation-free.  Not thread-safe against concurrent launches
+ * of the same plan. */
 int tcsc_gpu_plan_reserve(tcsc_gpu_plan *plan, int max_M);
 void tcsc_gpu_plan_destroy(tcsc_gpu_plan *plan);
 
@@ -96,7 +100,8 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan *plan);
  *        `cols` are not touched
  *   act: PReLU(v) = (v < 0 ? a*v : v) for the PRELU variants, identity
  *        otherwise.
- * Asynchronous on `stream`; no allocation, no synchronisation (safe to
+ * Asynchronous on `stream`; once the workspace covers M (see
+ * tcsc_gpu_plan_reserve) no allocation and no synchronisation (safe to
  * capture in a hipGraph). */
 int tcsc_gpu_sgemm(const tcsc_gpu_plan *plan, const float *dX, const float *dB,
                    float *dY, int M, int ldy, int variant, float a,

@@ -122,3 +122,73 @@ def test_gpu_entry_points_fail_loudly_without_device(built_lib):
     r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
     assert "no HIP device" in r.stderr
+
+
+# g++ (Itanium ABI) names the reference harness's objects reference: the
+# reference compiles its .c files as C++ without extern "C" (SURVEY.md §8b,
+# "Linkage"), so a link-level drop-in must export exactly these.
+REFERENCE_MANGLED = {
+    "_Z15tcsc_from_densePfii": "tcsc_from_dense",
+    "_Z16tcsc_sgemm_basicPfPK6tcsc_tS_S_iii": "tcsc_sgemm_basic",
+    "_Z20tcsc_sgemm_optimizedPfPK6tcsc_tS_S_iii": "tcsc_sgemm_optimized",
+    "_Z22tcsc_sgemm_prelu_basicPfPK6tcsc_tS_fS_iii": "tcsc_sgemm_prelu_basic",
+    "_Z35tcsc_sgemm_prelu_optimized_separatePfPK6tcsc_tS_fS_iii": "tcsc_sgemm_prelu_optimized_separate",
+    "_Z34tcsc_sgemm_prelu_optimized_onthegoPfPK6tcsc_tS_fS_iii": "tcsc_sgemm_prelu_optimized_onthego",
+    "_Z9tcsc_freeP6tcsc_t": "tcsc_free",
+    "_Z15init_rand_denseii": "init_rand_dense",
+    "_Z16init_rand_sparseiii": "init_rand_sparse",
+    "_Z7comparePfS_ii": "compare",
+    "_Z10gemm_basicPfS_S_S_iii": "gemm_basic",
+}
+
+
+def test_reference_mangled_names_are_exported(built_lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", tcsc_amd.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if l.strip()}
+    missing = sorted(set(REFERENCE_MANGLED) - exported)
+    assert not missing, missing
+
+
+def test_mangled_aliases_forward_to_c_entry_points(built_lib, monkeypatch):
+    """The C++-ABI alias of tcsc_from_dense builds the same TCSC as the C
+    name (host builder: no GPU), and compare() agrees."""
+    import ctypes
+
+    monkeypatch.setenv("TCSC_BUILDER", "host")
+    lib = ctypes.CDLL(tcsc_amd.LIB_PATH)
+    g = load_golden("cfg1")
+    Wd = np.ascontiguousarray(g["Wd"].astype(np.float32))
+    fp = ctypes.POINTER(ctypes.c_float)
+    K, N = Wd.shape
+    f_c = lib.tcsc_from_dense
+    f_x = getattr(lib, "_Z15tcsc_from_densePfii")
+    for f in (f_c, f_x):
+        f.restype = ctypes.c_void_p
+        f.argtypes = [fp, ctypes.c_int, ctypes.c_int]
+    pc = f_c(Wd.ctypes.data_as(fp), K, N)
+    px = f_x(Wd.ctypes.data_as(fp), K, N)
+    assert pc and px
+
+    class T(ctypes.Structure):
+        _fields_ = [("rows", ctypes.c_int), ("cols", ctypes.c_int), ("n_pos", ctypes.c_int), ("n_neg", ctypes.c_int),
+                    ("csp", ctypes.POINTER(ctypes.c_int)), ("csn", ctypes.POINTER(ctypes.c_int)),
+                    ("rip", ctypes.POINTER(ctypes.c_int)), ("rin", ctypes.POINTER(ctypes.c_int))]
+
+    a, b = T.from_address(pc), T.from_address(px)
+    assert (a.rows, a.cols, a.n_pos, a.n_neg) == (b.rows, b.cols, b.n_pos, b.n_neg)
+    assert np.array_equal(np.ctypeslib.as_array(a.rip, (a.n_pos,)), np.ctypeslib.as_array(b.rip, (b.n_pos,)))
+    assert np.array_equal(np.ctypeslib.as_array(a.rin, (a.n_neg,)), np.ctypeslib.as_array(b.rin, (b.n_neg,)))
+    free_x = getattr(lib, "_Z9tcsc_freeP6tcsc_t")
+    free_x.argtypes = [ctypes.c_void_p]
+    free_x(px)
+    lib.tcsc_free.argtypes = [ctypes.c_void_p]
+    lib.tcsc_free(pc)
+    cmp_x = getattr(lib, "_Z7comparePfS_ii")
+    cmp_x.restype = ctypes.c_bool
+    cmp_x.argtypes = [fp, fp, ctypes.c_int, ctypes.c_int]
+    y = np.ones((3, 5), np.float32)
+    z = y.copy()
+    assert cmp_x(y.ctypes.data_as(fp), z.ctypes.data_as(fp), 3, 5)
+    z[1, 2] += 1e-3
+    assert not cmp_x(y.ctypes.data_as(fp), z.ctypes.data_as(fp), 3, 5)
