@@ -18,15 +18,27 @@ constexpr int kTK = TCSC_TK;             // K rows per LDS chunk
 constexpr int kNBuf = TCSC_NBUF;         // LDS tile ring: chunk c in buffer c % kNBuf, kNBuf-1 chunks in flight
 constexpr int kRowBytes = kTM * 4;       // one LDS row = X[m0..m0+255][k], 1 KiB
 constexpr int kBufRows = kTK + 1;        // + one row of -0.0 that padding entries point at
-constexpr int kWaves = 8;                // waves per workgroup (1 workgroup per CU)
-constexpr int kCW = 32;                  // output columns per wave (4*kCW accumulator VGPRs)
-constexpr int kBatch = 8;                // stream entries per batch (pipeline step)
+// Gather geometry (tools/gen_gather_asm.py generates the matching loop):
+#ifndef TCSC_WAVES
+#define TCSC_WAVES 16
+#endif
+#ifndef TCSC_CW
+#define TCSC_CW 16
+#endif
+#ifndef TCSC_BATCH
+#define TCSC_BATCH 4
+#endif
+constexpr int kWaves = TCSC_WAVES;       // waves per workgroup (1 workgroup per CU; kWaves/4 per SIMD)
+constexpr int kCW = TCSC_CW;             // output columns per wave (4*kCW accumulator VGPRs)
+constexpr int kBatch = TCSC_BATCH;       // stream entries per batch (pipeline step, stream padding)
+constexpr int kWavesPerSimd = kWaves / 4;
+static_assert(kWaves % 4 == 0 && kWaves <= 16, "whole waves per SIMD");
 constexpr int kEntGuard = 64;            // entries allocated past the last stream (block loads)
 constexpr int kLdsBytes = kNBuf * kBufRows * kRowBytes;  // 147 KiB
 constexpr int kDmaPerWave = kTK / kWaves;                 // 1-KiB LDS-DMA rows per wave and chunk
 static_assert(kTK % kWaves == 0, "each wave DMAs the same number of rows");
 static_assert(kLdsBytes <= 160 * 1024, "LDS");
-static_assert(kNBuf == 3, "k_stream issues DMA(c+2) into the buffer chunk c-1 used");
+static_assert(kNBuf == 2 || kNBuf == 3, "ring of 2 (DMA(c+1) before gather(c)) or 3 (DMA(c+2) after it)");
 
 // Stream entry (8 bytes): word0 = +1.0f or -1.0f (bit pattern), word1 =
 // (lds_row << 10) | (4*slot); lds_row = (chunk%3)*kBufRows + (k - chunk*kTK)

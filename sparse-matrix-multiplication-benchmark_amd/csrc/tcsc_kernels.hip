@@ -149,12 +149,36 @@ __global__ void k_fill_pads(const int* __restrict__ cptr, const int* __restrict_
 
 // X (M x K, row-major) -> XT (K x ldxt), ldxt = M rounded up to kTM; the
 // rows m in [M, ldxt) are written as 0.  64x64 tiles through LDS (the +1
-// column makes both the row writes and the column reads conflict-free);
-// HBM-bound: 2*M*K*4 bytes per call.
+// column keeps the column reads conflict-free).  HBM-bound: 2*M*K*4 bytes
+// per call.  VEC (K % 4 == 0, X 16-B aligned): 16-B loads along k and
+// 16-B stores along m; otherwise scalar, guarded.
+template <bool VEC>
 __global__ void __launch_bounds__(256) k_transpose(const float* __restrict__ X, int M, int K, float* __restrict__ XT,
                                                    int ldxt) {
     __shared__ float t[64][65];
     const int k0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+    if (VEC) {
+        const int q = threadIdx.x & 15, rr = threadIdx.x >> 4;  // 16 float4 per 64-wide row
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = rr + 16 * i, m = m0 + r, k = k0 + 4 * q;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (m < M && k < K) v = *reinterpret_cast<const float4*>(X + (size_t)m * K + k);
+            t[r][4 * q + 0] = v.x;
+            t[r][4 * q + 1] = v.y;
+            t[r][4 * q + 2] = v.z;
+            t[r][4 * q + 3] = v.w;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int kk = rr + 16 * i, k = k0 + kk;
+            if (k < K)
+                *reinterpret_cast<float4*>(XT + (size_t)k * ldxt + m0 + 4 * q) =
+                    make_float4(t[4 * q + 0][kk], t[4 * q + 1][kk], t[4 * q + 2][kk], t[4 * q + 3][kk]);
+        }
+        return;
+    }
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -169,7 +193,13 @@ __global__ void __launch_bounds__(256) k_transpose(const float* __restrict__ X, 
     }
 }
 
+#ifdef TCSC_GATHER_INC
+#include TCSC_GATHER_INC
+#else
 #include "gather_asm.inc"
+#endif
+static_assert(TCSC_GEN_CW == kCW && TCSC_GEN_BATCH == kBatch, "generated loop geometry");
+static_assert(TCSC_GEN_BUDGET == (512 / kWavesPerSimd) / 8 * 8, "generated loop VGPR budget");
 
 // Consume this wave's stream for one chunk: `nb` batches of 8 entries at
 // `stream` (entries padded to a multiple of 8).  The chunk's first 64-entry
@@ -179,30 +209,19 @@ __global__ void __launch_bounds__(256) k_transpose(const float* __restrict__ X, 
 // whole chunk to land.  The schedule and register map are in
 // tools/gen_gather_asm.py.  s_set_gpr_idx_* writes M0, which the compiler
 // also uses (LDS-DMA destination): the asm saves it in s68 and restores it.
-#define TCSC_GATHER_CLOBBERS                                                                                        \
-    "memory", "scc", "v168", "v169", "v170", "v171", "v172", "v173", "v174", "v175", "v176", "v177", "v178", "v179",  \
-        "v180", "v181", "v182", "v183", "v184", "v185", "v186", "v187", "v188", "v189", "v190", "v191", "v192",       \
-        "v193", "v194", "v195", "v196", "v197", "v198", "v199", "v200", "v201", "v202", "v203", "v204", "v205",       \
-        "v206", "v207", "v208", "v209", "v210", "v211", "v212", "v213", "v214", "v215", "v216", "v217", "v218",       \
-        "v219", "v220", "v221", "v222", "v223", "v224", "v225", "v226", "v227", "v228", "v229", "v230", "v231",       \
-        "v234", "v235", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48",     \
-        "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63",       \
-        "s64", "s65", "s66", "s67", "s68"
-
 struct EntryRegs {
-    int s0, w0;  // pinned to v232/v233
-    int s1, w1;  // pinned to v238/v239
+    int s0, w0;  // pinned to pair A0 (TCSC_E0S/W)
+    int s1, w1;  // pinned to pair A1 (TCSC_E1S/W)
 };
 
 template <int PAR>
 __device__ __forceinline__ void gather_stream(const int2* __restrict__ stream, const int2* __restrict__ next,
-                                              unsigned nb, EntryRegs& er, unsigned lane, unsigned mask, f32x32& a0,
-                                              f32x32& a1, f32x32& a2, f32x32& a3) {
+                                              unsigned nb, EntryRegs& er, unsigned lane, unsigned mask,
+                                              f32x32 (&acc)[TCSC_ACC_VECS]) {
     unsigned voff = lane * 8u;  // byte offset of this lane's entry in a block
     asm volatile(TCSC_GATHER_ASM_0
-                 : [nb] "+s"(nb), "+{v[40:71]}"(a0), "+{v[72:103]}"(a1), "+{v[104:135]}"(a2),
-                   "+{v[136:167]}"(a3), "+{v232}"(er.s0), "+{v233}"(er.w0), "+{v238}"(er.s1), "+{v239}"(er.w1),
-                   "+{v236}"(voff)
+                 : [nb] "+s"(nb), TCSC_ACC_OPERANDS(acc), TCSC_E0S(er.s0), TCSC_E0W(er.w0), TCSC_E1S(er.s1),
+                   TCSC_E1W(er.w1), TCSC_VOFF(voff)
                  : [ent] "s"(stream), [nent] "s"(next), [lane] "v"(lane * 16u), [mask] "v"(mask)
                  : TCSC_GATHER_CLOBBERS);
 }
@@ -210,80 +229,101 @@ __device__ __forceinline__ void gather_stream(const int2* __restrict__ stream, c
 template <>
 __device__ __forceinline__ void gather_stream<1>(const int2* __restrict__ stream, const int2* __restrict__ next,
                                                  unsigned nb, EntryRegs& er, unsigned lane, unsigned mask,
-                                                 f32x32& a0, f32x32& a1, f32x32& a2, f32x32& a3) {
+                                                 f32x32 (&acc)[TCSC_ACC_VECS]) {
     unsigned voff = lane * 8u;
     asm volatile(TCSC_GATHER_ASM_1
-                 : [nb] "+s"(nb), "+{v[40:71]}"(a0), "+{v[72:103]}"(a1), "+{v[104:135]}"(a2),
-                   "+{v[136:167]}"(a3), "+{v232}"(er.s0), "+{v233}"(er.w0), "+{v238}"(er.s1), "+{v239}"(er.w1),
-                   "+{v236}"(voff)
+                 : [nb] "+s"(nb), TCSC_ACC_OPERANDS(acc), TCSC_E0S(er.s0), TCSC_E0W(er.w0), TCSC_E1S(er.s1),
+                   TCSC_E1W(er.w1), TCSC_VOFF(voff)
                  : [ent] "s"(stream), [nent] "s"(next), [lane] "v"(lane * 16u), [mask] "v"(mask)
                  : TCSC_GATHER_CLOBBERS);
 }
 
 // i is a compile-time constant after unrolling
-__device__ __forceinline__ float acc_get(const f32x32& a0, const f32x32& a1, const f32x32& a2, const f32x32& a3,
-                                         int i) {
-    return i < 32 ? a0[i] : (i < 64 ? a1[i - 32] : (i < 96 ? a2[i - 64] : a3[i - 96]));
-}
-__device__ __forceinline__ void acc_set(f32x32& a0, f32x32& a1, f32x32& a2, f32x32& a3, int i, float v) {
-    if (i < 32) a0[i] = v;
-    else if (i < 64) a1[i - 32] = v;
-    else if (i < 96) a2[i - 64] = v;
-    else a3[i - 96] = v;
+__device__ __forceinline__ float acc_get(const f32x32 (&acc)[TCSC_ACC_VECS], int i) { return acc[i >> 5][i & 31]; }
+__device__ __forceinline__ void acc_set(f32x32 (&acc)[TCSC_ACC_VECS], int i, float v) { acc[i >> 5][i & 31] = v; }
+
+// LDS-DMA of X^T chunks.  Row k of chunk c = XT[c*kTK + k][m0..m0+255] (1
+// KiB); wave w moves rows w*D .. w*D+D-1 (D = kDmaPerWave), lane l the 16 B
+// of rows m0+4l..4l+3.  Per-lane offsets are fixed for the whole kernel, so
+// a chunk costs D x (s_add m0 + global_load_lds_dwordx4) and one 64-bit base
+// advance.  X^T carries kNBuf-1 chunks of padding rows past the last chunk,
+// so the look-ahead never needs a clamp (those rows are never gathered).
+// M0 is not used by anything the compiler emits in this kernel; the gather
+// asm saves and restores it anyway.
+struct DmaState {
+    const char* next;              // byte address of the next chunk's first row, column m0
+    unsigned voff[kDmaPerWave];    // lane*16 + (w*D + i) * ldxt*4
+    unsigned lds_wave;             // LDS address of this wave's first row in buffer 0
+    size_t chunk_bytes;            // kTK * ldxt * 4
+};
+
+__device__ __forceinline__ void dma_next_chunk(DmaState& d, int buf) {
+#if !((defined(TCSC_ABLATION) && TCSC_ABLATION == 6) || defined(TCSC_NODMA))
+    const unsigned m0base = d.lds_wave + (unsigned)(buf * (kBufRows * kRowBytes));
+#pragma unroll
+    for (int i = 0; i < kDmaPerWave; ++i)
+        asm volatile("s_add_u32 m0, %0, %1\n\tglobal_load_lds_dwordx4 %2, %3"
+                     :
+                     : "s"(m0base), "n"(i * kRowBytes), "v"(d.voff[i]), "s"(d.next)
+                     : "memory", "scc");
+#endif
+    d.next += d.chunk_bytes;
 }
 
-// Issue this wave's LDS-DMA rows of chunk c (clamped to the last chunk, so
-// the look-ahead past the end stays branch-free) into ring buffer `buf`:
-// row k of the chunk = XT[k][m0..m0+255], one 1-KiB global_load_lds_dwordx4
-// per row (lane l moves rows m0+4l..4l+3).  kDmaPerWave VMEM ops per wave.
-__device__ __forceinline__ void dma_chunk(char* lds, const float* __restrict__ xcol, size_t ldxt, int K, int nch,
-                                          int c, int buf, int wave) {
-#if (defined(TCSC_ABLATION) && TCSC_ABLATION == 6) || defined(TCSC_NODMA)
-    return;  // timing only: no staging
-#endif
-    const int cc = min(c, nch - 1);
-    char* dst = lds + buf * (kBufRows * kRowBytes);
-#pragma unroll
-    for (int i = 0; i < kDmaPerWave; ++i) {
-        const int kl = wave * kDmaPerWave + i;
-        const int k = min(cc * kTK + kl, K - 1);
-        __builtin_amdgcn_global_load_lds(xcol + (size_t)k * ldxt, dst + kl * kRowBytes, 16, 0, 0);
-    }
+// XCD-aware tile order.  Workgroups are dealt round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md "Workgroup dispatch"; speed only, never correctness),
+// so launch order L puts L % 8 on one XCD.  Renumber so each XCD gets a
+// contiguous range of the (column block fastest, row tile, slice) order: the
+// ~32 workgroups an XCD runs at once then share one row tile of X^T, and its
+// L2 serves the rows they all stream.  Bijective for any grid size.
+struct Tile {
+    int cb, rt, z;
+};
+__device__ __forceinline__ Tile xcd_tile() {
+    const int ncb = gridDim.x, nrt = gridDim.y;
+    const int T = ncb * nrt * gridDim.z;
+    const int L = blockIdx.x + ncb * (blockIdx.y + nrt * blockIdx.z);
+    const int q = T >> 3, r = T & 7, x = L & 7;
+    const int Lg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
+    Tile t;
+    t.cb = Lg % ncb;
+    const int rest = Lg / ncb;
+    t.rt = rest % nrt;
+    t.z = rest / nrt;
+    return t;
 }
 
 // OUT: 0 = final Y (bias + activation), 1 = partial slab ws[slice][M][ncols]
 template <bool BIAS_FIRST, bool PRELU, int OUT>
-__global__ void __launch_bounds__(kWaves * 64, 2)
+__global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd)
 k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __restrict__ ent,
          const int* __restrict__ sptr, int G, int ncols, int nch, int chunks_per_slice, const float* __restrict__ Bias,
          float* __restrict__ Y, int ldy, float a, float* __restrict__ ws) {
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int g = blockIdx.x * kWaves + wave;  // wave-column group
-    const int m0 = blockIdx.y * kTM;
-    const int c_begin = blockIdx.z * chunks_per_slice;
+    const Tile t = xcd_tile();
+    const int g = t.cb * kWaves + wave;  // wave-column group
+    const int m0 = t.rt * kTM;
+    const int c_begin = t.z * chunks_per_slice;
     const int c_end = min(nch, c_begin + chunks_per_slice);
     const bool active = g < G;
 
-    f32x32 a0, a1, a2, a3;
+    f32x32 acc[TCSC_ACC_VECS];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-        a0[i] = 0.f;
-        a1[i] = 0.f;
-        a2[i] = 0.f;
-        a3[i] = 0.f;
-    }
+    for (int v = 0; v < TCSC_ACC_VECS; ++v)
+#pragma unroll
+        for (int i = 0; i < 32; ++i) acc[v][i] = 0.f;
     if (BIAS_FIRST && OUT == 0 && active) {
-        // one vector load of the wave's 32 bias values, then lane broadcasts
+        // one vector load of the wave's kCW bias values, then lane broadcasts
         // (keeps them out of the SGPRs the gather loop owns)
-        const int cb = g * kCW + (lane & (kCW - 1));
-        const float bv = cb < ncols ? Bias[cb] : 0.f;
+        const int cb = g * kCW + lane;
+        const float bv = (lane < kCW && cb < ncols) ? Bias[cb] : 0.f;
 #pragma unroll
         for (int j = 0; j < kCW; ++j) {
             const float b = __shfl(bv, j);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc_set(a0, a1, a2, a3, 4 * j + r, b);
+            for (int r = 0; r < 4; ++r) acc_set(acc, 4 * j + r, b);
         }
     }
 
@@ -294,20 +334,28 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     }
 
     if (c_begin < c_end) {
-        // Chunk c lives in ring buffer c % 3 (the plan baked that into every
-        // entry); DMA(c+2) is issued right after gather(c), so two chunks are
-        // in flight while one is consumed.  Per wave the VMEM order is
+        // Chunk c lives in ring buffer c % kNBuf (the plan baked that into
+        // every entry).  Ring of 3: DMA(c+2) is issued right after gather(c),
+        // so two chunks are in flight while one is consumed; per wave the
+        // VMEM order is
         //   ... DMA(c) | E(c) [+ block loads, waited inside] | DMA(c+1) | E(c+1) ...
         // (E = the chunk's first entry block, loaded by gather(c-1)), so at
         // the top of chunk c, vmcnt(kDmaPerWave) means DMA(c) and E(c) have
-        // landed; the barrier then makes every wave's rows of chunk c
-        // visible and says all waves are done reading chunk c-1's buffer,
-        // which DMA(c+2) reuses.  All loads in the loop are asm or LDS-DMA,
-        // so the compiler inserts no waits of its own.
-        const float* xcol = XT + m0 + 4 * lane;
-        const size_t ld = (size_t)ldxt;
+        // landed.  Ring of 2: DMA(c+1) is issued right after the barrier of
+        // chunk c (its buffer held chunk c-1), so it has gather(c) to land;
+        // the top of chunk c+1 waits vmcnt(0).  Either way the barrier makes
+        // every wave's rows of chunk c visible and says all waves are done
+        // with chunk c-1's buffer.  All loads in the loop are asm, so the
+        // compiler inserts no waits of its own.
+        DmaState dma;
+        dma.chunk_bytes = (size_t)kTK * ldxt * 4;
+        dma.next = reinterpret_cast<const char*>(XT + (size_t)c_begin * kTK * ldxt + m0);
+#pragma unroll
+        for (int i = 0; i < kDmaPerWave; ++i)
+            dma.voff[i] = 16u * lane + (unsigned)((wave * kDmaPerWave + i) * ldxt * 4);
+        dma.lds_wave = (unsigned)reinterpret_cast<uintptr_t>(lds) + (unsigned)(wave * kDmaPerWave * kRowBytes);
         int buf = c_begin % kNBuf;
-        dma_chunk(lds, xcol, ld, K, nch, c_begin, buf, wave);
+        dma_next_chunk(dma, buf);  // DMA(c_begin)
 
         const int gi = active ? g : G - 1;
         int cb = c_begin;
@@ -316,20 +364,22 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         int s0n = __builtin_amdgcn_readfirstlane(vs0);
         int s1n = __builtin_amdgcn_readfirstlane(vs1);
         EntryRegs er;
-        asm volatile("global_load_dwordx2 v[232:233], %2, %3"
-                     : "={v232}"(er.s0), "={v233}"(er.w0)
+        asm volatile("global_load_dwordx2 " TCSC_E0_PAIR ", %2, %3"
+                     : TCSC_E0S_OUT(er.s0), TCSC_E0W_OUT(er.w0)
                      : "v"(lane * 8u), "s"(ent + s0n)
                      : "memory");
         er.s1 = 0;
         er.w1 = 0;
-        dma_chunk(lds, xcol, ld, K, nch, c_begin + 1, buf == kNBuf - 1 ? 0 : buf + 1, wave);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // pad rows
+        if (kNBuf == 3) dma_next_chunk(dma, buf == 2 ? 0 : buf + 1);  // DMA(c_begin+1)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // pad rows
 
         const unsigned mask = 0x3ffu;
         auto chunk = [&](int c, bool valid, auto par) {
             constexpr int PAR = decltype(par)::value;
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDmaPerWave) : "memory");
+            // see the VMEM order above: ring of 3 keeps DMA(c+1) in flight
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kNBuf == 3 ? kDmaPerWave : 0) : "memory");
             __builtin_amdgcn_s_barrier();
+            if (kNBuf == 2) dma_next_chunk(dma, buf ^ 1);  // DMA(c+1) into the buffer chunk c-1 used
             const int s0 = s0n, s1 = s1n;
             const int idx = c + 1 - cb;
             if (idx == 64) {  // next 64 chunks' stream bounds
@@ -344,14 +394,16 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                 s1n = __builtin_amdgcn_readlane(vs1, idx);
             }
             const unsigned nb = (active && valid) ? (unsigned)(s1 - s0) / kBatch : 0u;
-            gather_stream<PAR>(ent + s0, ent + s0n, nb, er, lane, mask, a0, a1, a2, a3);
-            int b2 = buf + 2;
-            if (b2 >= kNBuf) b2 -= kNBuf;
-            dma_chunk(lds, xcol, ld, K, nch, c + 2, b2, wave);
+            gather_stream<PAR>(ent + s0, ent + s0n, nb, er, lane, mask, acc);
+            if (kNBuf == 3) {
+                int b2 = buf + 2;
+                if (b2 >= 3) b2 -= 3;
+                dma_next_chunk(dma, b2);  // DMA(c+2) into the buffer chunk c-1 used
+            }
             buf = buf == kNBuf - 1 ? 0 : buf + 1;
         };
         // unrolled by 2 for the entry-block parity; an odd chunk count runs
-        // one empty step (nb = 0; its DMA and look-ahead are clamped)
+        // one empty step (nb = 0; its DMA and look-ahead stay in the padding)
         for (int c = c_begin; c < c_end; c += 2) {
             chunk(c, true, std::integral_constant<int, 0>());
             chunk(c + 1, c + 1 < c_end, std::integral_constant<int, 1>());
@@ -363,35 +415,39 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     // Epilogue: lanes hold rows (4 per lane), so a direct store would put
     // 64 rows' 4-byte pieces in one instruction (partial-line writes that
     // cost ~16x the bytes in HBM writes).  Transpose through LDS instead:
-    // per half tile (128 rows) every wave parks its 128 x 32 block (16 KiB,
-    // row stride 128 B, 16-B quads XOR-swizzled by row/4 so the b128
-    // writes and reads spread over the banks), then reads it back as rows:
-    // 8 lanes per 128-B row segment, 16-B stores.
+    // per pass of kEpiRows rows every wave parks its kEpiRows x kCW block
+    // (row stride kCW*4 + 16 B, so the b128 writes of consecutive lanes,
+    // 4 rows apart, spread over the banks), then reads it back as rows:
+    // kCW/4 lanes per row, 16-B stores.
     __syncthreads();  // every wave is done with the tile ring
-    char* region = lds + wave * (128 * 128);
-    const int lh = lane & 31;
+    constexpr int kQ = kCW / 4;                 // 16-B quads per row
+    constexpr int kStride = kCW * 4 + 16;       // bytes per parked row
+    constexpr int kEpiRows = (kWaves * 128 * kStride <= kLdsBytes) ? 128 : 64;
+    static_assert(kWaves * kEpiRows * kStride <= kLdsBytes, "epilogue staging fits the LDS");
+    constexpr int kLanesPerPass = kEpiRows / 4;
+    constexpr int kRowsPerRead = 64 / kQ;       // rows one read instruction covers
+    char* region = lds + wave * (kEpiRows * kStride);
     const int col0 = g * kCW;
     const bool vec_ok = OUT == 0 ? ((ldy & 3) == 0 && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0))
                                  : ((ncols & 3) == 0 && ((reinterpret_cast<uintptr_t>(ws) & 15) == 0));
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        if (active && (lane >> 5) == h) {
+    for (int h = 0; h < 256 / kEpiRows; ++h) {
+        if (active && lane / kLanesPerPass == h) {
+            const int lh = lane % kLanesPerPass;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int R = 4 * lh + r;
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const float4 v = make_float4(acc_get(a0, a1, a2, a3, 4 * (4 * q + 0) + r),
-                                                 acc_get(a0, a1, a2, a3, 4 * (4 * q + 1) + r),
-                                                 acc_get(a0, a1, a2, a3, 4 * (4 * q + 2) + r),
-                                                 acc_get(a0, a1, a2, a3, 4 * (4 * q + 3) + r));
-                    *reinterpret_cast<float4*>(region + R * 128 + ((q ^ (lh & 7)) << 4)) = v;
+                for (int q = 0; q < kQ; ++q) {
+                    const float4 v = make_float4(acc_get(acc, 4 * (4 * q + 0) + r), acc_get(acc, 4 * (4 * q + 1) + r),
+                                                 acc_get(acc, 4 * (4 * q + 2) + r), acc_get(acc, 4 * (4 * q + 3) + r));
+                    *reinterpret_cast<float4*>(region + R * kStride + q * 16) = v;
                 }
             }
         }
         __syncthreads();
-        if (active) {
-            const int q = lane & 7;
+        if (active && lane < kRowsPerRead * kQ) {
+            const int q = lane % kQ;
             const int col = col0 + 4 * q;
             float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
             if (OUT == 0 && !BIAS_FIRST) {
@@ -401,10 +457,11 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                 bq.w = col + 3 < ncols ? Bias[col + 3] : 0.f;
             }
 #pragma unroll 4
-            for (int i = 0; i < 16; ++i) {
-                const int R = (lane >> 3) + 8 * i;
-                const int row = m0 + 128 * h + R;
-                float4 v = *reinterpret_cast<const float4*>(region + R * 128 + ((q ^ ((R >> 2) & 7)) << 4));
+            for (int i = 0; i < (kEpiRows + kRowsPerRead - 1) / kRowsPerRead; ++i) {
+                const int R = lane / kQ + kRowsPerRead * i;
+                const int row = m0 + kEpiRows * h + R;
+                if (R >= kEpiRows) break;
+                float4 v = *reinterpret_cast<const float4*>(region + R * kStride + q * 16);
                 if (row < M && col < ncols) {
                     float* dst;
                     if (OUT == 0) {
@@ -422,7 +479,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                         }
                         dst = Y + (size_t)row * ldy + col;
                     } else {
-                        dst = ws + ((size_t)blockIdx.z * M + row) * ncols + col;
+                        dst = ws + ((size_t)t.z * M + row) * ncols + col;
                     }
                     if (vec_ok && col + 3 < ncols) {
                         *reinterpret_cast<float4*>(dst) = v;
@@ -435,7 +492,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                 }
             }
         }
-        if (h == 0) __syncthreads();  // region reused by the second half
+        if (h + 1 < 256 / kEpiRows) __syncthreads();  // region reused by the next pass
     }
 }
 
@@ -551,9 +608,11 @@ size_t workspace_bytes(int M, int ncols, int slices) {
 
 static inline int ldxt_of(int M) { return (M + kTM - 1) / kTM * kTM; }
 
-// X^T of one call: K x ldxt floats, 256-B aligned size.
+// X^T of one call: (chunks + kNBuf-1 look-ahead chunks) * kTK rows of ldxt
+// floats (rows >= K are never gathered), 256-B aligned size.
 size_t xt_bytes(int M, int K) {
-    const size_t b = (size_t)K * ldxt_of(M) * sizeof(float);
+    const size_t rows = ((size_t)(K + kTK - 1) / kTK + kNBuf - 1) * kTK;
+    const size_t b = rows * ldxt_of(M) * sizeof(float);
     return (b + 255) / 256 * 256;
 }
 
@@ -618,8 +677,13 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
     if (g.K > 0) {
         if (!g.XT) return hipErrorInvalidValue;
         const int ldxt = ldxt_of(g.M);
-        hipLaunchKernelGGL(k_transpose, dim3((g.K + 63) / 64, ldxt / 64), dim3(256), 0, st, g.X, g.M, g.K, g.XT,
-                           ldxt);
+        const bool vec = (g.K % 4 == 0) && ((reinterpret_cast<uintptr_t>(g.X) & 15) == 0);
+        if (vec)
+            hipLaunchKernelGGL(k_transpose<true>, dim3((g.K + 63) / 64, ldxt / 64), dim3(256), 0, st, g.X, g.M, g.K,
+                               g.XT, ldxt);
+        else
+            hipLaunchKernelGGL(k_transpose<false>, dim3((g.K + 63) / 64, ldxt / 64), dim3(256), 0, st, g.X, g.M,
+                               g.K, g.XT, ldxt);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
