@@ -199,6 +199,7 @@ __global__ void __launch_bounds__(256) k_transpose(const float* __restrict__ X, 
 #include "gather_asm.inc"
 #endif
 static_assert(TCSC_GEN_CW == kCW && TCSC_GEN_BATCH == kBatch, "generated loop geometry");
+static_assert(TCSC_GEN_CAP <= kEntGuard, "stream prefetch stays inside the entry guard");
 static_assert(TCSC_GEN_BUDGET == (512 / kWavesPerSimd) / 8 * 8, "generated loop VGPR budget");
 
 // Consume this wave's stream for one chunk: `nb` batches of 8 entries at
@@ -209,33 +210,27 @@ static_assert(TCSC_GEN_BUDGET == (512 / kWavesPerSimd) / 8 * 8, "generated loop 
 // whole chunk to land.  The schedule and register map are in
 // tools/gen_gather_asm.py.  s_set_gpr_idx_* writes M0, which the compiler
 // also uses (LDS-DMA destination): the asm saves it in s68 and restores it.
-struct EntryRegs {
-    int s0, w0;  // pinned to pair A0 (TCSC_E0S/W)
-    int s1, w1;  // pinned to pair A1 (TCSC_E1S/W)
-};
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(4))) const i32x16 const_i32x16;
 
-template <int PAR>
-__device__ __forceinline__ void gather_stream(const int2* __restrict__ stream, const int2* __restrict__ next,
-                                              unsigned nb, EntryRegs& er, unsigned lane, unsigned mask,
-                                              f32x32 (&acc)[TCSC_ACC_VECS]) {
-    unsigned voff = lane * 8u;  // byte offset of this lane's entry in a block
-    asm volatile(TCSC_GATHER_ASM_0
-                 : [nb] "+s"(nb), TCSC_ACC_OPERANDS(acc), TCSC_E0S(er.s0), TCSC_E0W(er.w0), TCSC_E1S(er.s1),
-                   TCSC_E1W(er.w1), TCSC_VOFF(voff)
-                 : [ent] "s"(stream), [nent] "s"(next), [lane] "v"(lane * 16u), [mask] "v"(mask)
+// Consume this wave's stream for one chunk: `nb` batches of kBatch entries.
+// The first TCSC_GEN_CAP entries are already in the pinned SGPR buffer `sb`
+// (loaded by the caller's scalar loads); `ptr` is the stream's address, used
+// to reload the buffer for streams longer than the capacity.  The schedule
+// and register map are in tools/gen_gather_asm.py.
+__device__ __forceinline__ void gather_stream(unsigned nb, i32x16 (&sb)[TCSC_SBUF_VECS], unsigned long long ptr,
+                                              unsigned lane, unsigned mask, f32x32 (&acc)[TCSC_ACC_VECS]) {
+    asm volatile(TCSC_GATHER_ASM
+                 : [nb] "+s"(nb), TCSC_ACC_OPERANDS(acc), TCSC_SBUF_OPERANDS(sb), TCSC_PTR_OPERAND(ptr)
+                 : [lane] "v"(lane * 16u), [mask] "v"(mask)
                  : TCSC_GATHER_CLOBBERS);
 }
 
-template <>
-__device__ __forceinline__ void gather_stream<1>(const int2* __restrict__ stream, const int2* __restrict__ next,
-                                                 unsigned nb, EntryRegs& er, unsigned lane, unsigned mask,
-                                                 f32x32 (&acc)[TCSC_ACC_VECS]) {
-    unsigned voff = lane * 8u;
-    asm volatile(TCSC_GATHER_ASM_1
-                 : [nb] "+s"(nb), TCSC_ACC_OPERANDS(acc), TCSC_E0S(er.s0), TCSC_E0W(er.w0), TCSC_E1S(er.s1),
-                   TCSC_E1W(er.w1), TCSC_VOFF(voff)
-                 : [ent] "s"(stream), [nent] "s"(next), [lane] "v"(lane * 16u), [mask] "v"(mask)
-                 : TCSC_GATHER_CLOBBERS);
+// Scalar (SMEM) load of a stream's first TCSC_GEN_CAP entries.
+__device__ __forceinline__ void load_stream(i32x16 (&sb)[TCSC_SBUF_VECS], const int2* p) {
+    const_i32x16* q = reinterpret_cast<const_i32x16*>(reinterpret_cast<uintptr_t>(p));
+#pragma unroll
+    for (int i = 0; i < TCSC_SBUF_VECS; ++i) sb[i] = q[i];
 }
 
 // i is a compile-time constant after unrolling
@@ -248,8 +243,9 @@ __device__ __forceinline__ void acc_set(f32x32 (&acc)[TCSC_ACC_VECS], int i, flo
 // a chunk costs D x (s_add m0 + global_load_lds_dwordx4) and one 64-bit base
 // advance.  X^T carries kNBuf-1 chunks of padding rows past the last chunk,
 // so the look-ahead never needs a clamp (those rows are never gathered).
-// M0 is not used by anything the compiler emits in this kernel; the gather
-// asm saves and restores it anyway.
+// M0 is written in the same statement that reads it (the compiler keeps
+// nothing in M0 across statements), with the s_nop the M0 -> LDS-DMA hazard
+// asks for; the gather asm saves and restores it anyway.
 struct DmaState {
     const char* next;              // byte address of the next chunk's first row, column m0
     unsigned voff[kDmaPerWave];    // lane*16 + (w*D + i) * ldxt*4
@@ -262,7 +258,7 @@ __device__ __forceinline__ void dma_next_chunk(DmaState& d, int buf) {
     const unsigned m0base = d.lds_wave + (unsigned)(buf * (kBufRows * kRowBytes));
 #pragma unroll
     for (int i = 0; i < kDmaPerWave; ++i)
-        asm volatile("s_add_u32 m0, %0, %1\n\tglobal_load_lds_dwordx4 %2, %3"
+        asm volatile("s_add_u32 m0, %0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3"
                      :
                      : "s"(m0base), "n"(i * kRowBytes), "v"(d.voff[i]), "s"(d.next)
                      : "memory", "scc");
@@ -338,10 +334,9 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         // every entry).  Ring of 3: DMA(c+2) is issued right after gather(c),
         // so two chunks are in flight while one is consumed; per wave the
         // VMEM order is
-        //   ... DMA(c) | E(c) [+ block loads, waited inside] | DMA(c+1) | E(c+1) ...
-        // (E = the chunk's first entry block, loaded by gather(c-1)), so at
-        // the top of chunk c, vmcnt(kDmaPerWave) means DMA(c) and E(c) have
-        // landed.  Ring of 2: DMA(c+1) is issued right after the barrier of
+        //   ... DMA(c) | DMA(c+1) | ...
+        // so at the top of chunk c, vmcnt(kDmaPerWave) means DMA(c) has
+        // landed (entry streams are scalar loads, counted by lgkmcnt).  Ring of 2: DMA(c+1) is issued right after the barrier of
         // chunk c (its buffer held chunk c-1), so it has gather(c) to land;
         // the top of chunk c+1 waits vmcnt(0).  Either way the barrier makes
         // every wave's rows of chunk c visible and says all waves are done
@@ -363,19 +358,13 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         int vs0 = sptr[ci], vs1 = sptr[ci + 1];
         int s0n = __builtin_amdgcn_readfirstlane(vs0);
         int s1n = __builtin_amdgcn_readfirstlane(vs1);
-        EntryRegs er;
-        asm volatile("global_load_dwordx2 " TCSC_E0_PAIR ", %2, %3"
-                     : TCSC_E0S_OUT(er.s0), TCSC_E0W_OUT(er.w0)
-                     : "v"(lane * 8u), "s"(ent + s0n)
-                     : "memory");
-        er.s1 = 0;
-        er.w1 = 0;
+        i32x16 sb[TCSC_SBUF_VECS];
+        load_stream(sb, ent + s0n);
         if (kNBuf == 3) dma_next_chunk(dma, buf == 2 ? 0 : buf + 1);  // DMA(c_begin+1)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // pad rows
 
         const unsigned mask = 0x3ffu;
-        auto chunk = [&](int c, bool valid, auto par) {
-            constexpr int PAR = decltype(par)::value;
+        for (int c = c_begin; c < c_end; ++c) {
             // see the VMEM order above: ring of 3 keeps DMA(c+1) in flight
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kNBuf == 3 ? kDmaPerWave : 0) : "memory");
             __builtin_amdgcn_s_barrier();
@@ -393,20 +382,15 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                 s0n = __builtin_amdgcn_readlane(vs0, idx);
                 s1n = __builtin_amdgcn_readlane(vs1, idx);
             }
-            const unsigned nb = (active && valid) ? (unsigned)(s1 - s0) / kBatch : 0u;
-            gather_stream<PAR>(ent + s0, ent + s0n, nb, er, lane, mask, acc);
+            const unsigned nb = active ? (unsigned)(s1 - s0) / kBatch : 0u;
+            gather_stream(nb, sb, reinterpret_cast<unsigned long long>(ent + s0), lane, mask, acc);
+            load_stream(sb, ent + s0n);  // next chunk's stream: lands behind the DMA issue and the barrier
             if (kNBuf == 3) {
                 int b2 = buf + 2;
                 if (b2 >= 3) b2 -= 3;
                 dma_next_chunk(dma, b2);  // DMA(c+2) into the buffer chunk c-1 used
             }
             buf = buf == kNBuf - 1 ? 0 : buf + 1;
-        };
-        // unrolled by 2 for the entry-block parity; an odd chunk count runs
-        // one empty step (nb = 0; its DMA and look-ahead stay in the padding)
-        for (int c = c_begin; c < c_end; c += 2) {
-            chunk(c, true, std::integral_constant<int, 0>());
-            chunk(c + 1, c + 1 < c_end, std::integral_constant<int, 1>());
         }
         // no LDS-DMA may still be writing when the workgroup's LDS is released
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
