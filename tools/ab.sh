@@ -1,0 +1,10 @@
+#!/bin/bash
+# A/B timing of library builds in one session: ab.sh name=lib ... (alternating, 3 rounds)
+cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
+for r in 1 2 3; do
+  for spec in "$@"; do
+    n=${spec%%=*}; lib=${spec#*=}
+    TCSC_AMD_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err || { echo "$n failed"; tail -3 gpurun_out/ab_$n.err; exit 1; }
+    python -c "import json; d=json.load(open('gpurun_out/ab_$n.json')); print('round $r $n', round(d['roofline']['kernel_ms'],4), 'ms')"
+  done
+done
