@@ -107,6 +107,16 @@ int tcsc_gpu_sgemm(const tcsc_gpu_plan *plan, const float *dX, const float *dB,
                    float *dY, int M, int ldy, int variant, float a,
                    void *stream);
 
+/* The two halves of tcsc_gpu_sgemm, for callers that time them apart or
+ * reuse one staging of X for several launches of the same plan:
+ * tcsc_gpu_prepare_x writes X (M x K) transposed into the plan's workspace
+ * (kernel k_transpose); tcsc_gpu_sgemm_prepared then runs the gather
+ * (k_stream, plus k_reduce when K is split) on that staged X for the same
+ * M.  Same stream semantics as tcsc_gpu_sgemm. */
+int tcsc_gpu_prepare_x(const tcsc_gpu_plan *plan, const float *dX, int M, void *stream);
+int tcsc_gpu_sgemm_prepared(const tcsc_gpu_plan *plan, const float *dB, float *dY, int M, int ldy,
+                            int variant, float a, void *stream);
+
 /* Device-side tcsc_from_dense: dense K x N row-major float matrix on the
  * device -> TCSC arrays on the device, bit-exact with the reference builder
  * (tcsc.c:6-66).  Two calls: first with the four output pointers NULL to

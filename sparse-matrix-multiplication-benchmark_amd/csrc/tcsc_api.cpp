@@ -199,13 +199,13 @@ class DeviceGuard {
 
 namespace {
 int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy, int variant,
-             float a, void* stream, float* ws, size_t ws_bytes) {
-    if (!p || M < 0 || ldy < p->cols || variant < 0 || variant > 4) {
+             float a, void* stream, float* ws, size_t ws_bytes, int stage = 0) {
+    if (!p || M < 0 || (stage != 1 && (ldy < p->cols || variant < 0 || variant > 4))) {
         set_error("tcsc_gpu_sgemm: bad arguments (M=%d ldy=%d variant=%d)", M, ldy, variant);
         return TCSC_E_ARG;
     }
     if (M == 0 || p->cols == 0) return TCSC_OK;
-    if (!dY || !dB || (!dX && p->rows > 0)) {
+    if ((stage != 1 && (!dY || !dB)) || (stage != 2 && !dX && p->rows > 0)) {
         set_error("tcsc_gpu_sgemm: NULL device pointer");
         return TCSC_E_ARG;
     }
@@ -231,6 +231,7 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
     g.ws = (ws && ws_bytes > xtb) ? reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + xtb) : nullptr;
     g.ws_bytes = g.ws ? ws_bytes - xtb : 0;
     g.force_slices = slices_override();
+    g.stage = stage;
     // Bias first for tcsc_sgemm_basic (tcsc.c:74-96), last otherwise
     // (tcsc.c:149-161; the optimized family adds per-sign partial sums to
     // the bias, which no single accumulation order reproduces: DESIGN.md).
@@ -372,6 +373,25 @@ int tcsc_gpu_sgemm(const tcsc_gpu_plan* p, const float* dX, const float* dB, flo
         if (rc != TCSC_OK) return rc;
     }
     return sgemm_ws(p, dX, dB, dY, M, ldy, variant, a, stream, p ? p->ws : nullptr, p ? p->ws_bytes : 0);
+}
+
+static int ensure_workspace(const tcsc_gpu_plan* p, int M) {
+    if (p && M > 0 && p->cols > 0 && p->ws_bytes < wanted_workspace(p, M))
+        return tcsc_gpu_plan_reserve(const_cast<tcsc_gpu_plan*>(p), M);
+    return TCSC_OK;
+}
+
+int tcsc_gpu_prepare_x(const tcsc_gpu_plan* p, const float* dX, int M, void* stream) {
+    const int rc = ensure_workspace(p, M);
+    if (rc != TCSC_OK) return rc;
+    return sgemm_ws(p, dX, nullptr, nullptr, M, 0, 0, 0.f, stream, p ? p->ws : nullptr, p ? p->ws_bytes : 0, 1);
+}
+
+int tcsc_gpu_sgemm_prepared(const tcsc_gpu_plan* p, const float* dB, float* dY, int M, int ldy, int variant, float a,
+                            void* stream) {
+    const int rc = ensure_workspace(p, M);
+    if (rc != TCSC_OK) return rc;
+    return sgemm_ws(p, nullptr, dB, dY, M, ldy, variant, a, stream, p ? p->ws : nullptr, p ? p->ws_bytes : 0, 2);
 }
 
 int tcsc_gpu_from_dense(const float* d_dense, int rows, int cols, int* d_csp, int* d_csn, int* d_rip, int* d_rin,

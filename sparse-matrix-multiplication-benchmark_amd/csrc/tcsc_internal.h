@@ -92,7 +92,8 @@ struct GemmArgs {
     bool prelu = false;
     float* ws = nullptr;       // split-K partial slabs (may be null: no split)
     size_t ws_bytes = 0;
-    int force_slices = 0;      // 0 = cost model
+    int force_slices = 0;
+    int stage = 0;             // 0: transpose + gather, 1: transpose only, 2: gather only (X^T prepared)      // 0 = cost model
 };
 
 // Plan building

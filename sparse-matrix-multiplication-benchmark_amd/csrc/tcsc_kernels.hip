@@ -658,7 +658,7 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
 // workspace, ahead of the split-K slabs in g.ws).
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
     if (g.M <= 0 || g.ncols <= 0) return hipSuccess;
-    if (g.K > 0) {
+    if (g.K > 0 && g.stage != 2) {
         if (!g.XT) return hipErrorInvalidValue;
         const int ldxt = ldxt_of(g.M);
         const bool vec = (g.K % 4 == 0) && ((reinterpret_cast<uintptr_t>(g.X) & 15) == 0);
@@ -671,6 +671,7 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
+    if (g.stage == 1) return hipSuccess;
     const int s = choose_slices(g.M, g.ncols, g.K, g.nnz, g.n_groups, g.ws ? g.ws_bytes : 0, g.force_slices);
     if (g.bias_first) return g.prelu ? launch_t<true, true>(g, s, st) : launch_t<true, false>(g, s, st);
     return g.prelu ? launch_t<false, true>(g, s, st) : launch_t<false, false>(g, s, st);

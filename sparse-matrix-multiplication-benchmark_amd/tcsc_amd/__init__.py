@@ -38,7 +38,8 @@ EXPORTED_SYMBOLS = (
     "tcsc_set_seed",
     # include/tcsc_gpu.h
     "tcsc_gpu_device_count", "tcsc_gpu_plan_create", "tcsc_gpu_plan_create_device", "tcsc_gpu_plan_get_info",
-    "tcsc_gpu_plan_reserve", "tcsc_gpu_plan_destroy", "tcsc_gpu_sgemm", "tcsc_gpu_from_dense", "tcsc_gpu_last_error",
+    "tcsc_gpu_plan_reserve", "tcsc_gpu_plan_destroy", "tcsc_gpu_sgemm", "tcsc_gpu_prepare_x",
+    "tcsc_gpu_sgemm_prepared", "tcsc_gpu_from_dense", "tcsc_gpu_last_error",
     "tcsc_gpu_cache_clear", "tcsc_gpu_num_shards", "tcsc_gpu_set_num_shards",
 )
 
@@ -107,6 +108,8 @@ def lib():
     L.tcsc_gpu_plan_destroy.argtypes = [vp]
     L.tcsc_gpu_plan_destroy.restype = None
     L.tcsc_gpu_sgemm.argtypes = [vp, vp, vp, vp, i, i, i, f, vp]
+    L.tcsc_gpu_prepare_x.argtypes = [vp, vp, i, vp]
+    L.tcsc_gpu_sgemm_prepared.argtypes = [vp, vp, vp, i, i, i, f, vp]
     L.tcsc_gpu_from_dense.argtypes = [vp, i, i, vp, vp, vp, vp, C.POINTER(i), C.POINTER(i), vp]
     L.tcsc_gpu_num_shards.restype = i
     L.tcsc_gpu_set_num_shards.argtypes = [i]
@@ -255,7 +258,7 @@ class Plan:
         return {k: getattr(inf, k) for k, _ in plan_info_t._fields_}
 
     def reserve(self, max_M: int) -> None:
-        """Allocate the split-K workspace for launches of up to max_M rows."""
+        """Allocate the workspace (X^T + split-K slabs) for launches of up to max_M rows."""
         _check(lib().tcsc_gpu_plan_reserve(self.handle, int(max_M)), "tcsc_gpu_plan_reserve")
 
     def sgemm(self, X, B, Y, M: int, ldy: int, variant: str = "prelu_basic", a: float = 0.2,
@@ -263,6 +266,18 @@ class Plan:
         _check(lib().tcsc_gpu_sgemm(self.handle, C.c_void_p(_ptr(X)), C.c_void_p(_ptr(B)), C.c_void_p(_ptr(Y)),
                                     int(M), int(ldy), VARIANT_ID[variant], float(a), C.c_void_p(stream)),
                "tcsc_gpu_sgemm")
+
+    def prepare_x(self, X, M: int, stream: int = 0) -> None:
+        """First half of sgemm: stage X^T in the plan's workspace (k_transpose)."""
+        _check(lib().tcsc_gpu_prepare_x(self.handle, C.c_void_p(_ptr(X)), int(M), C.c_void_p(stream)),
+               "tcsc_gpu_prepare_x")
+
+    def sgemm_prepared(self, B, Y, M: int, ldy: int, variant: str = "prelu_basic", a: float = 0.2,
+                       stream: int = 0) -> None:
+        """Second half of sgemm: the gather on the staged X^T (k_stream)."""
+        _check(lib().tcsc_gpu_sgemm_prepared(self.handle, C.c_void_p(_ptr(B)), C.c_void_p(_ptr(Y)), int(M), int(ldy),
+                                             VARIANT_ID[variant], float(a), C.c_void_p(stream)),
+               "tcsc_gpu_sgemm_prepared")
 
     def destroy(self) -> None:
         if getattr(self, "handle", None):

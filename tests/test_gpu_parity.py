@@ -105,6 +105,34 @@ def test_device_api_matches_host_api(gpu, torch_cuda, oracle):
     plan.destroy()
 
 
+@pytest.mark.parametrize("name", ["cfg1", "edge_k_not_mult4", "edge_long_k"])
+def test_prepare_then_gather_equals_sgemm(gpu, torch_cuda, name):
+    """tcsc_gpu_prepare_x + tcsc_gpu_sgemm_prepared == tcsc_gpu_sgemm, bit for
+    bit, and one staged X^T serves several gathers."""
+    torch = torch_cuda
+    g = load_golden(name)
+    W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
+    dev = torch.device("cuda:0")
+    X = torch.from_numpy(np.ascontiguousarray(g["X"])).to(dev)
+    B = torch.from_numpy(g["B"]).to(dev)
+    M, N = g["X"].shape[0], W.cols
+    stream = torch.cuda.current_stream().cuda_stream
+    plan = tcsc_amd.Plan(W, 0, N, 0, stream)
+    plan.reserve(M)
+    Y1 = torch.empty((M, N), device=dev)
+    plan.sgemm(X, B, Y1, M, N, "prelu_basic", 0.2, stream)
+    plan.prepare_x(X, M, stream)
+    for variant in ("prelu_basic", "basic"):
+        Y2 = torch.empty((M, N), device=dev)
+        plan.sgemm_prepared(B, Y2, M, N, variant, 0.2, stream)
+        Y3 = torch.empty((M, N), device=dev)
+        plan.sgemm(X, B, Y3, M, N, variant, 0.2, stream)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(Y2.cpu().numpy(), Y3.cpu().numpy())
+    torch.cuda.synchronize()
+    plan.destroy()
+
+
 @pytest.mark.parametrize("shards", [2, 3, 5])
 def test_multi_shard_host_path_equals_single(gpu, shards):
     """The column-block path (one block per GPU on a node; several blocks

@@ -1,0 +1,15 @@
+#!/bin/bash
+# HBM traffic of k_stream per launch (MI355X_MICROARCH.md "HBM"): FETCH_SIZE
+# and WRITE_SIZE in separate --pmc passes (they cannot share one), kernel
+# trace only; tools/traffic_json.py applies the gfx950 x2 FETCH_SIZE
+# correction and writes profiles/traffic.json for bench.py.
+cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp; mkdir -p gpurun_out
+B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
+i=0
+for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  rm -rf gpurun_out/traffic$i
+  timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d gpurun_out/traffic$i -o run -- $B > gpurun_out/traffic$i.log 2>&1
+  rc=$?; echo "pass $i ($set) rc=$rc"; [ $rc -ne 0 ] && exit $rc
+done
+# profiles/traffic.json: run `python tools/traffic_json.py` after gpurun merged gpurun_out/ back

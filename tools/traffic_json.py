@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Per-launch HBM bytes of k_stream from the tools/traffic.sh passes.
+
+FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE
+counts half the bytes of 16-B-per-lane streaming reads (the LDS-DMA of X^T
+is exactly that), so it is doubled (MI355X_MICROARCH.md "HBM"); WRITE_SIZE
+is exact for the kernel's 16-B row stores.  Writes profiles/traffic.json
+keyed like bench.py looks it up ("cfg4:prelu_basic:16384").  Run it where
+gpurun_out/ holds the passes (here, after gpurun merged them back)."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_dispatch(root, counter, kernel="k_stream"):
+    vals = collections.defaultdict(float)
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    out = os.path.join(ROOT, "gpurun_out")
+    fetch = per_dispatch(os.path.join(out, "traffic1"), "FETCH_SIZE")
+    write = per_dispatch(os.path.join(out, "traffic2"), "WRITE_SIZE")
+    hit = per_dispatch(os.path.join(out, "traffic3"), "TCC_HIT_sum")
+    miss = per_dispatch(os.path.join(out, "traffic3"), "TCC_MISS_sum")
+    if not fetch or not write:
+        print("no k_stream dispatches found", file=sys.stderr)
+        return 1
+    f_kib = sum(fetch) / len(fetch)
+    w_kib = sum(write) / len(write)
+    rec = {
+        "kernel": "k_stream",
+        "fetch_size_kib_raw": f_kib,
+        "write_size_kib": w_kib,
+        "hbm_bytes_per_launch": (2.0 * f_kib + w_kib) * 1024.0,
+        "correction": "FETCH_SIZE x2 (gfx950, 16-B/lane streaming reads), WRITE_SIZE as is",
+        "l2_hit_rate": (sum(hit) / (sum(hit) + sum(miss))) if hit and miss else None,
+        "dispatches": [len(fetch), len(write)],
+    }
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    data = {}
+    if os.path.exists(path):
+        data = json.load(open(path))
+    key = os.environ.get("TRAFFIC_KEY", "cfg4:prelu_basic:16384")
+    data[key] = rec
+    json.dump(data, open(path, "w"), indent=1)
+    print(key, json.dumps(rec))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
