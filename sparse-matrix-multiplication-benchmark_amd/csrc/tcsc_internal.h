@@ -35,8 +35,19 @@ constexpr int kWavesPerSimd = kWaves / 4;
 static_assert(kWaves % 4 == 0 && kWaves <= 16, "whole waves per SIMD");
 constexpr int kEntGuard = 64;            // entries allocated past the last stream (block loads)
 constexpr int kLdsBytes = kNBuf * kBufRows * kRowBytes;  // 147 KiB
-constexpr int kDmaPerWave = kTK / kWaves;                 // 1-KiB LDS-DMA rows per wave and chunk
-static_assert(kTK % kWaves == 0, "each wave DMAs the same number of rows");
+// Staging: waves 0..kDmaWaves-1 move a chunk, kDmaPerWave 1-KiB rows each,
+// right after the chunk loop's barrier (TCSC_DMA_EARLY=1) or after their
+// gather (0).
+#ifndef TCSC_DMA_WAVES
+#define TCSC_DMA_WAVES TCSC_WAVES
+#endif
+#ifndef TCSC_DMA_EARLY
+#define TCSC_DMA_EARLY 0
+#endif
+constexpr int kDmaWaves = TCSC_DMA_WAVES;
+constexpr bool kDmaEarly = TCSC_DMA_EARLY != 0;
+constexpr int kDmaPerWave = kTK / kDmaWaves;              // 1-KiB LDS-DMA rows per DMA wave and chunk
+static_assert(kDmaWaves <= kWaves && kTK % kDmaWaves == 0, "each DMA wave moves the same number of rows");
 static_assert(kLdsBytes <= 160 * 1024, "LDS");
 static_assert(kNBuf == 2 || kNBuf == 3, "ring of 2 (DMA(c+1) before gather(c)) or 3 (DMA(c+2) after it)");
 

@@ -349,8 +349,9 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         for (int i = 0; i < kDmaPerWave; ++i)
             dma.voff[i] = 16u * lane + (unsigned)((wave * kDmaPerWave + i) * ldxt * 4);
         dma.lds_wave = (unsigned)reinterpret_cast<uintptr_t>(lds) + (unsigned)(wave * kDmaPerWave * kRowBytes);
+        const bool dma_wave = wave < kDmaWaves;  // uniform
         int buf = c_begin % kNBuf;
-        dma_next_chunk(dma, buf);  // DMA(c_begin)
+        if (dma_wave) dma_next_chunk(dma, buf);  // DMA(c_begin)
 
         const int gi = active ? g : G - 1;
         int cb = c_begin;
@@ -360,15 +361,49 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         int s1n = __builtin_amdgcn_readfirstlane(vs1);
         i32x16 sb[TCSC_SBUF_VECS];
         load_stream(sb, ent + s0n);
-        if (kNBuf == 3) dma_next_chunk(dma, buf == 2 ? 0 : buf + 1);  // DMA(c_begin+1)
+        if (kNBuf == 3 && dma_wave) dma_next_chunk(dma, buf == 2 ? 0 : buf + 1);  // DMA(c_begin+1)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // pad rows
 
         const unsigned mask = 0x3ffu;
+#ifdef TCSC_STAMPS
+        // diagnostic build: shader-clock stamps around the waits (outputs are garbage)
+        unsigned long long st_bar = 0, st_dma = 0, st_smem = 0, st_gather = 0, st_t0 = __builtin_amdgcn_s_memtime();
+#endif
+#ifdef TCSC_TRACE
+        // diagnostic build: for kTraceN intervals from c_begin + kTrace0, per wave {top, barrier
+        // release, stream landed, gather end, batches, HW_ID}, parked in LDS (no VMEM in the
+        // loop) and copied into Y at the end (outputs are garbage)
+        constexpr int kTrace0 = 100, kTraceN = 32;
+        __shared__ unsigned trace_lds[kTraceN * kWaves * 6];
+        const unsigned hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
         for (int c = c_begin; c < c_end; ++c) {
+#ifdef TCSC_STAMPS
+            const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
+#endif
+#ifdef TCSC_TRACE
+            const unsigned tr0 = (unsigned)__builtin_amdgcn_s_memtime();
+#endif
             // see the VMEM order above: ring of 3 keeps DMA(c+1) in flight
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kNBuf == 3 ? kDmaPerWave : 0) : "memory");
+#ifdef TCSC_STAMPS
+            const unsigned long long tbm = __builtin_amdgcn_s_memtime();
+            st_dma += tbm - tb0;
+#endif
             __builtin_amdgcn_s_barrier();
-            if (kNBuf == 2) dma_next_chunk(dma, buf ^ 1);  // DMA(c+1) into the buffer chunk c-1 used
+#ifdef TCSC_STAMPS
+            const unsigned long long tb1 = __builtin_amdgcn_s_memtime();
+            st_bar += tb1 - tbm;
+#endif
+#ifdef TCSC_TRACE
+            const unsigned tr1 = (unsigned)__builtin_amdgcn_s_memtime();
+#endif
+            if (kNBuf == 2 && dma_wave) dma_next_chunk(dma, buf ^ 1);  // DMA(c+1) into the buffer chunk c-1 used
+            if (kNBuf == 3 && kDmaEarly && dma_wave) {
+                int b2 = buf + 2;
+                if (b2 >= 3) b2 -= 3;
+                dma_next_chunk(dma, b2);  // DMA(c+2) into the buffer chunk c-1 used (free since the barrier)
+            }
             const int s0 = s0n, s1 = s1n;
             const int idx = c + 1 - cb;
             if (idx == 64) {  // next 64 chunks' stream bounds
@@ -383,17 +418,69 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                 s1n = __builtin_amdgcn_readlane(vs1, idx);
             }
             const unsigned nb = active ? (unsigned)(s1 - s0) / kBatch : 0u;
+#ifdef TCSC_STAMPS
+            const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[36:51]}"(sb[0]), "+{s[52:67]}"(sb[1]), "+{s[68:83]}"(sb[2]));
+            const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+            st_smem += ts1 - ts0;
+#endif
+#ifdef TCSC_TRACE
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[36:51]}"(sb[0]), "+{s[52:67]}"(sb[1]), "+{s[68:83]}"(sb[2]));
+            const unsigned trs = (unsigned)__builtin_amdgcn_s_memtime();
+#endif
             gather_stream(nb, sb, reinterpret_cast<unsigned long long>(ent + s0), lane, mask, acc);
+#ifdef TCSC_STAMPS
+            st_gather += __builtin_amdgcn_s_memtime() - ts1;
+#endif
+#ifdef TCSC_TRACE
+            {
+                const unsigned tr2 = (unsigned)__builtin_amdgcn_s_memtime();
+                const int ti = c - c_begin - kTrace0;
+                if (lane == 0 && ti >= 0 && ti < kTraceN) {
+                    unsigned* o = trace_lds + (ti * kWaves + wave) * 6;
+                    o[0] = tr0;
+                    o[1] = tr1;
+                    o[2] = trs;
+                    o[3] = tr2;
+                    o[4] = nb;
+                    o[5] = hwid;
+                }
+            }
+#endif
             load_stream(sb, ent + s0n);  // next chunk's stream: lands behind the DMA issue and the barrier
-            if (kNBuf == 3) {
+            if (kNBuf == 3 && !kDmaEarly && dma_wave) {
                 int b2 = buf + 2;
                 if (b2 >= 3) b2 -= 3;
                 dma_next_chunk(dma, b2);  // DMA(c+2) into the buffer chunk c-1 used
             }
             buf = buf == kNBuf - 1 ? 0 : buf + 1;
         }
+#ifdef TCSC_STAMPS
+        const unsigned long long st_total = __builtin_amdgcn_s_memtime() - st_t0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (lane == 0) {
+            const size_t wg = blockIdx.x + gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
+            unsigned* o = reinterpret_cast<unsigned*>(Y) + (wg * kWaves + wave) * 5;
+            o[0] = (unsigned)st_total;
+            o[1] = (unsigned)st_bar;
+            o[2] = (unsigned)st_smem;
+            o[3] = (unsigned)st_gather;
+            o[4] = (unsigned)st_dma;
+        }
+        return;
+#endif
         // no LDS-DMA may still be writing when the workgroup's LDS is released
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef TCSC_TRACE
+        {
+            unsigned* o = reinterpret_cast<unsigned*>(Y) +
+                          ((blockIdx.x + gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z)) * kWaves + wave) *
+                              (size_t)kTraceN * 6;
+            for (int i = lane; i < kTraceN * 6; i += 64) o[i] = trace_lds[((i / 6) * kWaves + wave) * 6 + i % 6];
+        }
+        return;  // Y holds the trace
+#endif
     }
 
     // Epilogue: lanes hold rows (4 per lane), so a direct store would put

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Generate the gather loop of kernel K1 (k_stream) for one register geometry.
 
-    gen_gather_asm.py [--cw 16] [--batch 4] [--cap 24] [--budget 128] [-o path]
+    gen_gather_asm.py [--cw 16] [--batch 4] [--cap 24] [--budget 128] [--depth 1] [-o path]
 
 Why generated: the loop is a fully unrolled, software-pipelined sequence of
 positions whose register names are static per position; writing it by hand
@@ -24,8 +24,9 @@ Per batch p (BATCH entries, slots j = BATCH*p + i of the phase):
             s_set_gpr_idx_on/idx word (low 8 bits = 4*slot) then two
             v_pk_fma_f32 acc[slot] += sign * x (DST and SRC2 relatively
             addressed), s_set_gpr_idx_off.
-Position p does ISSUE(p) then FMA(p-1), so a batch's LDS latency hides under
-the previous batch's FMAs.  X quads alternate between two register sets.
+Position p does ISSUE(p) then FMA(p-DEPTH), so a batch's LDS latency hides
+under the FMAs of the DEPTH batches before it (DEPTH*BATCH reads stay in
+flight).  X quads cycle through DEPTH+1 register sets.
 
 TCSC_ABLATION = 1..5 selects timing-only variants (wrong results):
 1 no index mode, 3 no LDS read, 4 no FMA, 5 no gather.
@@ -36,15 +37,17 @@ import sys
 
 
 class Geo:
-    def __init__(self, cw, batch, cap, budget):
+    def __init__(self, cw, batch, cap, budget, depth=1):
         assert cw % 8 == 0 and cap % batch == 0 and 36 + 2 * cap <= 100
-        self.cw, self.batch, self.cap, self.budget = cw, batch, cap, budget
+        assert 1 <= depth and depth * batch <= 15, "lgkmcnt counts to 15"
+        self.cw, self.batch, self.cap, self.budget, self.depth = cw, batch, cap, budget, depth
         self.npos = cap // batch
-        nacc, nx = 4 * cw, 8 * batch
-        self.xbase = (budget - nx) & ~3
+        assert self.npos > depth
+        nacc, self.nx = 4 * cw, 4 * batch * (depth + 1)
+        self.xbase = (budget - self.nx) & ~3
         self.acc = (self.xbase - nacc) & ~1
-        assert self.acc >= 24, "VGPR budget too small for this geometry"
-        self.xset = {0: self.xbase, 1: self.xbase + 4 * batch}
+        assert self.acc >= 12, "VGPR budget too small for this geometry"
+        self.xset = {k: self.xbase + 4 * batch * k for k in range(depth + 1)}
         self.sbase = 36
         self.slast = 36 + 2 * cap - 1
 
@@ -58,7 +61,7 @@ def sreg(g, j, w):
 
 
 def issue(g, p):
-    x = g.xset[p % 2]
+    x = g.xset[p % (g.depth + 1)]
     out = []
     for i in range(g.batch):
         out.append(f"v_bfi_b32 v{x + 4 * i}, %[mask], %[lane], s{sreg(g, g.batch * p + i, 1)}")
@@ -69,7 +72,7 @@ def issue(g, p):
 
 
 def fma(g, p, wait):
-    x = g.xset[p % 2]
+    x = g.xset[p % (g.depth + 1)]
     out = [f"s_waitcnt lgkmcnt({wait})"]
     if ABL == 4:
         return out
@@ -87,8 +90,10 @@ def fma(g, p, wait):
     return out
 
 
-def count(target):
-    return ["s_sub_u32 %[nb], %[nb], 1", "s_cmp_eq_u32 %[nb], 0", f"s_cbranch_scc1 {target}"]
+def count(p, target):
+    """After ISSUE(p): was batch p the phase's last one?  (nb is the number
+    of batches left in this phase and beyond; 2 SALU, no decrement.)"""
+    return [f"s_cmp_eq_u32 %[nb], {p + 1}", f"s_cbranch_scc1 {target}"]
 
 
 def reload(g):
@@ -112,21 +117,30 @@ def reload(g):
 def generate(g):
     if ABL == 5:
         return []
+    D = g.depth
+
+    def drain(last):
+        """FMA the batches still in flight after ISSUE(last), oldest first."""
+        out = []
+        for q in range(max(0, last - D + 1), last + 1):
+            out += fma(g, q, g.batch * (last - q))
+        return out
+
     L = ["s_cmp_eq_u32 %[nb], 0", "s_cbranch_scc1 .Lend%="]
     L.append(".Lphase%=:")
-    L += issue(g, 0)
-    L += count(".Ldrain0%=")
-    for p in range(1, g.npos):
+    for p in range(g.npos):
         L += issue(g, p)
-        L += fma(g, p - 1, g.batch)
-        L += count(f".Ldrain{p}%=")
-    # a full phase done with batches left: finish its last batch, reload, go on
-    L += fma(g, g.npos - 1, 0)
+        if p >= D:
+            L += fma(g, p - D, g.batch * D)
+        L += count(p, f".Ldrain{p}%=")
+    # a full phase done with batches left: finish its batches, reload, go on
+    L += drain(g.npos - 1)
+    L.append(f"s_sub_u32 %[nb], %[nb], {g.npos}")
     L += reload(g)
     L.append("s_branch .Lphase%=")
     for p in range(g.npos):
         L.append(f".Ldrain{p}%=:")
-        L += fma(g, p, 0)
+        L += drain(p)
         if p != g.npos - 1:
             L.append("s_branch .Lend%=")
     L.append(".Lend%=:")
@@ -147,8 +161,8 @@ def write_inc(path, g):
     assert (2 * g.cap) % 16 == 0
     with open(path, "w") as f:
         f.write("// GENERATED by tools/gen_gather_asm.py -- do not edit by hand.\n")
-        f.write(f"// geometry: cw={g.cw} batch={g.batch} cap={g.cap} vgpr budget={g.budget}: "
-                f"acc v[{g.acc}:{g.acc + 4 * g.cw - 1}], X v[{g.xbase}:{g.xbase + 8 * g.batch - 1}], "
+        f.write(f"// geometry: cw={g.cw} batch={g.batch} cap={g.cap} vgpr budget={g.budget} depth={g.depth}: "
+                f"acc v[{g.acc}:{g.acc + 4 * g.cw - 1}], X v[{g.xbase}:{g.xbase + g.nx - 1}], "
                 f"stream s[{g.sbase}:{g.slast}]\n")
         f.write(f"#define TCSC_GEN_CW {g.cw}\n#define TCSC_GEN_BATCH {g.batch}\n#define TCSC_GEN_CAP {g.cap}\n")
         f.write(f"#define TCSC_GEN_BUDGET {g.budget}\n#define TCSC_ACC_VECS {nvec}\n#define TCSC_SBUF_VECS {nsv}\n")
@@ -159,7 +173,7 @@ def write_inc(path, g):
         ptr = g.slast + 1 + ((g.slast + 1) & 1)
         f.write(f'#define TCSC_PTR_OPERAND(p) "+{{s[{ptr}:{ptr + 1}]}}"(p)\n')
         clob = ['"memory"', '"scc"']
-        clob += [f'"v{r}"' for r in range(g.xbase, g.xbase + 8 * g.batch)]
+        clob += [f'"v{r}"' for r in range(g.xbase, g.xbase + g.nx)]
         f.write("#define TCSC_GATHER_CLOBBERS " + ", ".join(clob) + "\n")
         f.write("#if !defined(TCSC_ABLATION) || TCSC_ABLATION == 0 || TCSC_ABLATION >= 6\n")
         for a in (0, 1, 3, 4, 5):
@@ -177,11 +191,12 @@ def main():
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--cap", type=int, default=24)
     ap.add_argument("--budget", type=int, default=128)
+    ap.add_argument("--depth", type=int, default=1)
     here = os.path.dirname(os.path.abspath(__file__))
     ap.add_argument("-o", default=os.path.join(here, "..", "sparse-matrix-multiplication-benchmark_amd", "csrc",
                                                "gather_asm.inc"))
     a = ap.parse_args()
-    write_inc(a.o, Geo(a.cw, a.batch, a.cap, a.budget))
+    write_inc(a.o, Geo(a.cw, a.batch, a.cap, a.budget, a.depth))
     print(a.o)
 
 
