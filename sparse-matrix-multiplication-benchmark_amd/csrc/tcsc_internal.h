@@ -37,9 +37,12 @@ constexpr int kEntGuard = 64;            // entries allocated past the last stre
 constexpr int kLdsBytes = kNBuf * kBufRows * kRowBytes;  // 147 KiB
 // Staging: waves 0..kDmaWaves-1 move a chunk, kDmaPerWave 1-KiB rows each,
 // right after the chunk loop's barrier (TCSC_DMA_EARLY=1) or after their
-// gather (0).
+// gather (0).  Default: the first half of the waves.  The SIMD arbiter
+// favours older waves (tools/trace.py: waves 0-3 finish their gathers first,
+// 12-15 last), so the DMA issue (~100 cycles per row) lands on waves with
+// slack at the barrier instead of on the critical path (A/B: -2.5 %).
 #ifndef TCSC_DMA_WAVES
-#define TCSC_DMA_WAVES TCSC_WAVES
+#define TCSC_DMA_WAVES (TCSC_WAVES / 2)
 #endif
 #ifndef TCSC_DMA_EARLY
 #define TCSC_DMA_EARLY 0

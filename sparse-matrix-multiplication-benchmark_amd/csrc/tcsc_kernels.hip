@@ -218,11 +218,17 @@ typedef __attribute__((address_space(4))) const i32x16 const_i32x16;
 // (loaded by the caller's scalar loads); `ptr` is the stream's address, used
 // to reload the buffer for streams longer than the capacity.  The schedule
 // and register map are in tools/gen_gather_asm.py.
+// `tptr` is the next chunk's stream: its first scalar-cache lines are
+// touched at the start (loads into the pinned `junk` SGPR, never read), so
+// the real s_load after this gather hits in K$.  Whoever runs after the loop
+// must wait lgkmcnt(0) before the junk register is released.
 __device__ __forceinline__ void gather_stream(unsigned nb, i32x16 (&sb)[TCSC_SBUF_VECS], unsigned long long ptr,
-                                              unsigned lane, unsigned mask, f32x32 (&acc)[TCSC_ACC_VECS]) {
+                                              const void* tptr, int& junk, unsigned lane, unsigned mask,
+                                              f32x32 (&acc)[TCSC_ACC_VECS]) {
     asm volatile(TCSC_GATHER_ASM
-                 : [nb] "+s"(nb), TCSC_ACC_OPERANDS(acc), TCSC_SBUF_OPERANDS(sb), TCSC_PTR_OPERAND(ptr)
-                 : [lane] "v"(lane * 16u), [mask] "v"(mask)
+                 : [nb] "+s"(nb), TCSC_ACC_OPERANDS(acc), TCSC_SBUF_OPERANDS(sb), TCSC_PTR_OPERAND(ptr),
+                   TCSC_JUNK_OPERAND(junk)
+                 : [lane] "v"(lane * 16u), [mask] "v"(mask), [tptr] "s"(tptr)
                  : TCSC_GATHER_CLOBBERS);
 }
 
@@ -365,6 +371,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // pad rows
 
         const unsigned mask = 0x3ffu;
+        int junk = 0;  // sink of the scalar-cache touches (gather_stream)
 #ifdef TCSC_STAMPS
         // diagnostic build: shader-clock stamps around the waits (outputs are garbage)
         unsigned long long st_bar = 0, st_dma = 0, st_smem = 0, st_gather = 0, st_t0 = __builtin_amdgcn_s_memtime();
@@ -428,7 +435,16 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
             asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[36:51]}"(sb[0]), "+{s[52:67]}"(sb[1]), "+{s[68:83]}"(sb[2]));
             const unsigned trs = (unsigned)__builtin_amdgcn_s_memtime();
 #endif
-            gather_stream(nb, sb, reinterpret_cast<unsigned long long>(ent + s0), lane, mask, acc);
+#if defined(TCSC_PRIO) && TCSC_PRIO
+            // longest stream first: the SIMD arbiter favours older waves, so a
+            // young wave with the most batches would otherwise finish last and
+            // hold the next barrier (tools/trace.py: gather time grows with slot)
+            if (nb >= (unsigned)(TCSC_PRIO + 2)) __builtin_amdgcn_s_setprio(3);
+            else if (nb >= (unsigned)(TCSC_PRIO + 1)) __builtin_amdgcn_s_setprio(2);
+            else if (nb >= (unsigned)TCSC_PRIO) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+#endif
+            gather_stream(nb, sb, reinterpret_cast<unsigned long long>(ent + s0), ent + s0n, junk, lane, mask, acc);
 #ifdef TCSC_STAMPS
             st_gather += __builtin_amdgcn_s_memtime() - ts1;
 #endif
@@ -470,8 +486,9 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         }
         return;
 #endif
-        // no LDS-DMA may still be writing when the workgroup's LDS is released
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // no LDS-DMA may still be writing when the workgroup's LDS is released,
+        // and no scalar-cache touch may land in the junk SGPR after its release
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+s"(junk)::"memory");
 #ifdef TCSC_TRACE
         {
             unsigned* o = reinterpret_cast<unsigned*>(Y) +

@@ -37,10 +37,11 @@ import sys
 
 
 class Geo:
-    def __init__(self, cw, batch, cap, budget, depth=1):
+    def __init__(self, cw, batch, cap, budget, depth=1, touch=4):
         assert cw % 8 == 0 and cap % batch == 0 and 36 + 2 * cap <= 100
         assert 1 <= depth and depth * batch <= 15, "lgkmcnt counts to 15"
         self.cw, self.batch, self.cap, self.budget, self.depth = cw, batch, cap, budget, depth
+        self.touch = touch  # scalar-cache lines of the NEXT chunk's stream touched at the start
         self.npos = cap // batch
         assert self.npos > depth
         nacc, self.nx = 4 * cw, 4 * batch * (depth + 1)
@@ -126,7 +127,16 @@ def generate(g):
             out += fma(g, q, g.batch * (last - q))
         return out
 
-    L = ["s_cmp_eq_u32 %[nb], 0", "s_cbranch_scc1 .Lend%="]
+    L = []
+    # Warm the scalar cache with the next chunk's stream (its start is known
+    # here), so the real s_load after this gather hits in K$ instead of
+    # paying an L2 round trip on the critical path after the barrier.  The
+    # loads land in the junk SGPR (pinned, never read); while they are in
+    # flight the lgkmcnt waits below are conservative, never wrong.
+    for t in range(g.touch):
+        off = min(64 * t, 8 * g.cap - 4)
+        L.append(f"s_load_dword %[junk], %[tptr], {hex(off)}")
+    L += ["s_cmp_eq_u32 %[nb], 0", "s_cbranch_scc1 .Lend%="]
     L.append(".Lphase%=:")
     for p in range(g.npos):
         L += issue(g, p)
@@ -172,6 +182,11 @@ def write_inc(path, g):
         f.write(f"#define TCSC_SBUF_OPERANDS(sb) {sops}\n")
         ptr = g.slast + 1 + ((g.slast + 1) & 1)
         f.write(f'#define TCSC_PTR_OPERAND(p) "+{{s[{ptr}:{ptr + 1}]}}"(p)\n')
+        if g.touch:
+            f.write(f'#define TCSC_JUNK_OPERAND(j) [junk] "+{{s{ptr + 2}}}"(j)\n')
+        else:
+            f.write('#define TCSC_JUNK_OPERAND(j) [junk] "+s"(j)\n')
+        f.write(f"#define TCSC_GEN_TOUCH {g.touch}\n")
         clob = ['"memory"', '"scc"']
         clob += [f'"v{r}"' for r in range(g.xbase, g.xbase + g.nx)]
         f.write("#define TCSC_GATHER_CLOBBERS " + ", ".join(clob) + "\n")
@@ -192,11 +207,12 @@ def main():
     ap.add_argument("--cap", type=int, default=24)
     ap.add_argument("--budget", type=int, default=128)
     ap.add_argument("--depth", type=int, default=1)
+    ap.add_argument("--touch", type=int, default=0)
     here = os.path.dirname(os.path.abspath(__file__))
     ap.add_argument("-o", default=os.path.join(here, "..", "sparse-matrix-multiplication-benchmark_amd", "csrc",
                                                "gather_asm.inc"))
     a = ap.parse_args()
-    write_inc(a.o, Geo(a.cw, a.batch, a.cap, a.budget, a.depth))
+    write_inc(a.o, Geo(a.cw, a.batch, a.cap, a.budget, a.depth, a.touch))
     print(a.o)
 
 
