@@ -52,6 +52,7 @@ def parse():
                    help="time only rank 0's block of an S-way strong split (per-GPU view of S GPUs)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-dense-baseline", action="store_true", help="skip the rocBLAS dense comparison (N=1 only)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
     p.add_argument("--override", default="", help="experiments only: e.g. 'K=16448,N=4096' (marks the line)")
     return p.parse_args()
@@ -106,7 +107,7 @@ def main():
     rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
     rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
     tcsc_amd.gpu_from_dense(inp["Wd"], cfg.K, ncols, csp, csn, rip, rin, stream=sh)
-    del inp["Wd"]
+    Wd = inp.pop("Wd") if (world == 1 and not args.no_dense_baseline) else None  # kept for the dense baseline
     plan = tcsc_amd.Plan.from_device(cfg.K, ncols, csp, csn, rip, rin, 0, ncols, local_rank, sh)
     plan.reserve(cfg.M)
     nnz = npos + nneg
@@ -215,6 +216,24 @@ def main():
                 "valu_add_frac": (adds_per_launch / gather_s) / VALU_ADD_PEAK,
             },
         }
+        if Wd is not None:
+            # the reference's "TCSC vs Dense" line (main.cpp:379-391) on the
+            # device -- gemm_basic's dense product with the same ternary W as an fp32 rocBLAS
+            # SGEMM + the bias/PReLU epilogue, same X, B and Y, timed with HIP events
+            Yd = torch.empty_like(Y)
+
+            def dense_step():
+                tcsc_amd.dense_sgemm(X, Wd, B, Yd, cfg.M, ncols, cfg.K, ncols, variant, 0.2, sh)
+
+            dense_step()
+            dense_s = timed(dense_step, 3)
+            out["dense_baseline"] = {
+                "kernel": "rocblas_sgemm fp32 (dense ternary W) + k_bias_act",
+                "ms": dense_s * 1e3,
+                "dense_tflops": 2.0 * cfg.M * cfg.K * ncols / dense_s / 1e12,
+                "tcsc_speedup": dense_s / (elapsed_max / args.steps),
+            }
+            del Yd
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, cfg, variant, X, B, csp, csn, rip[:npos], rin[:nneg])
         print(json.dumps(out), flush=True)

@@ -127,6 +127,19 @@ int tcsc_gpu_from_dense(const float *d_dense, int rows, int cols,
                         int *d_row_index_pos, int *d_row_index_neg,
                         int *n_pos, int *n_neg, void *stream);
 
+/* Dense baseline, the device counterpart of the
+ * reference's gemm_basic (dense/dense.c:64-77) that the harness times for
+ * its "TCSC vs Dense" line (main.cpp:379-391):
+ *   Y[m, n] = act(sum_k X[m,k] * W[k,n] + B[n])
+ * with W the DENSE K x N row-major float matrix (the ternary W before
+ * tcsc_from_dense), computed as an fp32 rocBLAS SGEMM plus a bias/PReLU
+ * epilogue kernel.  act as in tcsc_gpu_sgemm (PReLU for the PRELU
+ * variants).  dX: M x K row-major; dY: M rows of pitch ldy >= N.
+ * Asynchronous on `stream`. */
+int tcsc_gpu_dense_sgemm(const float *dX, const float *dW, const float *dB,
+                         float *dY, int M, int N, int K, int ldy, int variant,
+                         float a, void *stream);
+
 /* Message for the last failing call on this thread ("" if none). */
 const char *tcsc_gpu_last_error(void);
 

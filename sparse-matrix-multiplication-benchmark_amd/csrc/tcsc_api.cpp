@@ -11,6 +11,7 @@
 // unless TCSC_ON_ERROR=continue -- aborts, because silently leaving Y
 // unwritten would be worse than the reference's behaviour.
 #include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
 
 #include <cstdarg>
 #include <cstdio>
@@ -423,6 +424,57 @@ int tcsc_gpu_from_dense(const float* d_dense, int rows, int cols, int* d_csp, in
         HIP_TRY(tcsc::dense_to_tcsc_fill(d_dense, rows, cols, d_csp, d_csn, d_rip, d_rin, st));
         HIP_TRY(hipStreamSynchronize(st));
     }
+    return TCSC_OK;
+}
+
+// Dense baseline: the reference's gemm_basic
+// (dense/dense.c:64-77, y = sum_k X[m,k] W[k,n], then + B[n]) on the device:
+// rocBLAS fp32 SGEMM with the dense ternary W, then the bias (+PReLU)
+// epilogue kernel.  Row-major Y = X W is the column-major product
+// Y^T (N x M, ld ldy) = W^T (N x K, ld N) * X^T (K x M, ld K).
+int tcsc_gpu_dense_sgemm(const float* dX, const float* dW, const float* dB, float* dY, int M, int N, int K,
+                         int ldy, int variant, float a, void* stream) {
+    if (M < 0 || N < 0 || K < 0 || ldy < N || variant < 0 || variant > 4 ||
+        ((long long)M * N > 0 && (!dX || !dW || !dB || !dY))) {
+        set_error("tcsc_gpu_dense_sgemm: bad arguments (M=%d N=%d K=%d ldy=%d variant=%d)", M, N, K, ldy, variant);
+        return TCSC_E_ARG;
+    }
+    if (M == 0 || N == 0) return TCSC_OK;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    static std::mutex mu;
+    static std::unordered_map<int, rocblas_handle> handles;
+    rocblas_handle h = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = handles.find(dev);
+        if (it == handles.end()) {
+            if (rocblas_create_handle(&h) != rocblas_status_success) {
+                set_error("tcsc_gpu_dense_sgemm: rocblas_create_handle failed");
+                return TCSC_E_HIP;
+            }
+            handles[dev] = h;
+        } else {
+            h = it->second;
+        }
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (rocblas_set_stream(h, st) != rocblas_status_success) {
+        set_error("tcsc_gpu_dense_sgemm: rocblas_set_stream failed");
+        return TCSC_E_HIP;
+    }
+    const float one = 1.0f, zero = 0.0f;
+    if (K == 0) {
+        HIP_TRY(hipMemset2DAsync(dY, (size_t)ldy * sizeof(float), 0, (size_t)N * sizeof(float), M, st));
+    } else {
+        const rocblas_status rs = rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, N, M, K, &one, dW,
+                                                N, dX, K, &zero, dY, ldy);
+        if (rs != rocblas_status_success) {
+            set_error("tcsc_gpu_dense_sgemm: rocblas_sgemm failed (%s)", rocblas_status_to_string(rs));
+            return TCSC_E_HIP;
+        }
+    }
+    HIP_TRY(tcsc::launch_bias_act(dY, M, N, ldy, dB, variant >= TCSC_VARIANT_PRELU_BASIC, a, st));
     return TCSC_OK;
 }
 

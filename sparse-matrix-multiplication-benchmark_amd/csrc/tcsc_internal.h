@@ -123,6 +123,8 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st);
 hipError_t dense_to_tcsc_counts(const float* D, int rows, int cols, int* cntp, int* cntn, hipStream_t st);
 hipError_t dense_to_tcsc_fill(const float* D, int rows, int cols, const int* csp, const int* csn, int* rip,
                               int* rin, hipStream_t st);
+// Y[m, n] = act(Y[m, n] + B[n]) in place (the dense baseline's epilogue)
+hipError_t launch_bias_act(float* Y, int M, int N, int ldy, const float* B, bool prelu, float a, hipStream_t st);
 hipError_t exclusive_scan_i32(const int* in, int* out, int n, void* tmp, size_t tmp_bytes, hipStream_t st);
 
 }  // namespace tcsc

@@ -601,6 +601,41 @@ __global__ void k_reduce(const float* __restrict__ ws, int slices, int M, int nc
     }
 }
 
+// Dense-baseline epilogue (gemm_basic order, dense/dense.c:64-77: the bias
+// after the sum): Y = act(Y + B), one float4 of a row per thread where the
+// row pitch allows, HBM-bound (2*M*N*4 bytes).
+template <bool PRELU>
+__global__ void k_bias_act(float* __restrict__ Y, int M, int N, int ldy, const float* __restrict__ B, float a) {
+    const int nq = (N + 3) / 4;
+    const long long total = (long long)M * nq;
+    const bool vec = (ldy & 3) == 0 && (N & 3) == 0 && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0);
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int m = (int)(i / nq), n = 4 * (int)(i % nq);
+        float* y = Y + (size_t)m * ldy + n;
+        if (vec) {
+            float4 v = *reinterpret_cast<float4*>(y);
+            v.x += B[n + 0];
+            v.y += B[n + 1];
+            v.z += B[n + 2];
+            v.w += B[n + 3];
+            if (PRELU) {
+                v.x = (v.x < 0.0f) ? a * v.x : v.x;
+                v.y = (v.y < 0.0f) ? a * v.y : v.y;
+                v.z = (v.z < 0.0f) ? a * v.z : v.z;
+                v.w = (v.w < 0.0f) ? a * v.w : v.w;
+            }
+            *reinterpret_cast<float4*>(y) = v;
+        } else {
+            for (int j = 0; j < 4 && n + j < N; ++j) {
+                float v = y[j] + B[n + j];
+                if (PRELU) v = (v < 0.0f) ? a * v : v;
+                y[j] = v;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Device tcsc_from_dense (bit-exact with tcsc.c:6-66): per-column counts,
 // exclusive scans, then a fill that keeps rows ascending inside a column.
@@ -789,6 +824,16 @@ hipError_t dense_to_tcsc_counts(const float* D, int rows, int cols, int* cntp, i
 hipError_t dense_to_tcsc_fill(const float* D, int rows, int cols, const int* csp, const int* csn, int* rip, int* rin,
                               hipStream_t st) {
     hipLaunchKernelGGL(k_dense_fill, dim3(grid_for(cols, 256)), dim3(256), 0, st, D, rows, cols, csp, csn, rip, rin);
+    return hipGetLastError();
+}
+
+hipError_t launch_bias_act(float* Y, int M, int N, int ldy, const float* B, bool prelu, float a, hipStream_t st) {
+    const long long total = (long long)M * ((N + 3) / 4);
+    if (total == 0) return hipSuccess;
+    if (prelu)
+        hipLaunchKernelGGL(k_bias_act<true>, dim3(grid_for(total, 256)), dim3(256), 0, st, Y, M, N, ldy, B, a);
+    else
+        hipLaunchKernelGGL(k_bias_act<false>, dim3(grid_for(total, 256)), dim3(256), 0, st, Y, M, N, ldy, B, a);
     return hipGetLastError();
 }
 

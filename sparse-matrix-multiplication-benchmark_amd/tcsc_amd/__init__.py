@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     # include/tcsc_gpu.h
     "tcsc_gpu_device_count", "tcsc_gpu_plan_create", "tcsc_gpu_plan_create_device", "tcsc_gpu_plan_get_info",
     "tcsc_gpu_plan_reserve", "tcsc_gpu_plan_destroy", "tcsc_gpu_sgemm", "tcsc_gpu_prepare_x",
-    "tcsc_gpu_sgemm_prepared", "tcsc_gpu_from_dense", "tcsc_gpu_last_error",
+    "tcsc_gpu_sgemm_prepared", "tcsc_gpu_from_dense", "tcsc_gpu_dense_sgemm", "tcsc_gpu_last_error",
     "tcsc_gpu_cache_clear", "tcsc_gpu_num_shards", "tcsc_gpu_set_num_shards",
 )
 
@@ -111,6 +111,7 @@ def lib():
     L.tcsc_gpu_prepare_x.argtypes = [vp, vp, i, vp]
     L.tcsc_gpu_sgemm_prepared.argtypes = [vp, vp, vp, i, i, i, f, vp]
     L.tcsc_gpu_from_dense.argtypes = [vp, i, i, vp, vp, vp, vp, C.POINTER(i), C.POINTER(i), vp]
+    L.tcsc_gpu_dense_sgemm.argtypes = [vp, vp, vp, vp, i, i, i, i, i, f, vp]
     L.tcsc_gpu_num_shards.restype = i
     L.tcsc_gpu_set_num_shards.argtypes = [i]
     L.tcsc_gpu_set_num_shards.restype = None
@@ -289,6 +290,15 @@ class Plan:
             self.destroy()
         except Exception:
             pass
+
+
+def dense_sgemm(X, Wd, B, Y, M: int, N: int, K: int, ldy: int, variant: str = "prelu_basic", a: float = 0.2,
+                stream: int = 0) -> None:
+    """Dense baseline on the device (gemm_basic, dense/dense.c:64-77): Y = act(X Wd + B), rocBLAS fp32 SGEMM
+    plus the bias/PReLU epilogue kernel.  X, Wd, B, Y are device buffers (torch tensors or raw pointers)."""
+    _check(lib().tcsc_gpu_dense_sgemm(C.c_void_p(_ptr(X)), C.c_void_p(_ptr(Wd)), C.c_void_p(_ptr(B)),
+                                      C.c_void_p(_ptr(Y)), int(M), int(N), int(K), int(ldy), VARIANT_ID[variant],
+                                      float(a), C.c_void_p(stream)), "tcsc_gpu_dense_sgemm")
 
 
 def gpu_from_dense(d_dense, rows: int, cols: int, d_csp, d_csn, d_rip=None, d_rin=None, stream: int = 0):

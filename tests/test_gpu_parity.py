@@ -105,6 +105,29 @@ def test_device_api_matches_host_api(gpu, torch_cuda, oracle):
     plan.destroy()
 
 
+@pytest.mark.parametrize("name", ["cfg1", "cfg1_int", "edge_k_not_mult4", "edge_ragged_n65", "edge_m1"])
+def test_dense_baseline_matches_reference(gpu, torch_cuda, oracle, name):
+    """the dense GPU baseline (rocBLAS fp32 + bias/PReLU
+    epilogue) against the reference outputs: bit-exact on integer inputs,
+    the fp32 bound on float inputs; ldy > N padding untouched."""
+    torch = torch_cuda
+    g = load_golden(name)
+    dev = torch.device("cuda:0")
+    M, K = g["X"].shape
+    N = g["Wd"].shape[1]
+    X = torch.from_numpy(np.ascontiguousarray(g["X"])).to(dev)
+    Wd = torch.from_numpy(np.ascontiguousarray(g["Wd"].astype(np.float32))).to(dev)
+    B = torch.from_numpy(g["B"]).to(dev)
+    for variant in ("basic", "prelu_basic"):
+        Y = torch.full((M, N + 3), 7.0, device=dev)
+        tcsc_amd.dense_sgemm(X, Wd, B, Y, M, N, K, N + 3, variant, float(g["a"]),
+                             torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        out = Y.cpu().numpy()
+        assert np.all(out[:, N:] == 7.0)
+        check_variant(g, variant, np.ascontiguousarray(out[:, :N]), oracle)
+
+
 @pytest.mark.parametrize("name", ["cfg1", "edge_k_not_mult4", "edge_long_k"])
 def test_prepare_then_gather_equals_sgemm(gpu, torch_cuda, name):
     """tcsc_gpu_prepare_x + tcsc_gpu_sgemm_prepared == tcsc_gpu_sgemm, bit for
