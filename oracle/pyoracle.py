@@ -25,6 +25,9 @@ ORACLE_SO = os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libtcsc_ref.so")
 
 VARIANTS = ("basic", "optimized", "prelu_basic", "prelu_separate", "prelu_onthego")
+# the five bcsr_sgemm_* of sparse/bcsr.h:16-39, in the variant-id order of include/bcsr_gpu.h
+BCSR_VARIANTS = ("basic", "prelu_basic", "avx", "prelu_avx", "avx2")
+BCSR_PRELU_VARIANTS = ("prelu_basic", "prelu_avx")
 PRELU_VARIANTS = ("prelu_basic", "prelu_separate", "prelu_onthego")
 
 _f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
@@ -79,6 +82,44 @@ class TCSC:
         )
 
 
+@dataclass
+class BCSR:
+    """Host BCSR arrays (the fields of bcsr_t, sparse/bcsr.h:7-12).
+    b_row_start has br+1 entries; the ones past the reference's written
+    prefix (non-empty block rows + 1, bcsr.c:114-117,137) are k."""
+
+    r: int
+    c: int
+    br: int
+    bc: int
+    b_row_start: np.ndarray
+    b_col_idx: np.ndarray
+    b_values: np.ndarray  # k*r*c float32
+
+    @property
+    def k(self) -> int:
+        return int(self.b_col_idx.size)
+
+    def arrays(self):
+        return (self.b_row_start, self.b_col_idx, self.b_values)
+
+    def equal(self, other: "BCSR") -> bool:
+        return ((self.r, self.c, self.br, self.bc) == (other.r, other.c, other.br, other.bc)
+                and np.array_equal(self.b_row_start, other.b_row_start)
+                and np.array_equal(self.b_col_idx, other.b_col_idx)
+                and np.array_equal(self.b_values.view(np.uint32), other.b_values.view(np.uint32)))
+
+
+def bcsr_variant_allowed(variant: str, r: int, c: int, N: int) -> bool:
+    """Shapes each reference variant is defined for (and runs without
+    faulting: the avx forms use aligned 8-float loads, bcsr.c:229,250-256)."""
+    if variant in ("basic", "prelu_basic"):
+        return True
+    if c != 8 or N % 8:
+        return False
+    return variant != "avx2" or r == 8
+
+
 def _nz(a: np.ndarray) -> np.ndarray:
     """ctypes ndpointer rejects size-0 arrays' NULL data on some numpy builds."""
     return a if a.size else np.zeros(1, dtype=a.dtype)
@@ -112,6 +153,11 @@ class Oracle:
         L.oracle_fill_uniform.argtypes = [_f32p, C.c_size_t, C.c_uint64]
         L.oracle_fill_int.argtypes = [_f32p, C.c_size_t, C.c_uint64, C.c_int]
         L.oracle_fill_ternary.argtypes = [_f32p, C.c_size_t, C.c_uint64, C.c_double]
+        L.oracle_bcsr_count.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int),
+                                        C.POINTER(C.c_int)]
+        L.oracle_bcsr_fill.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.c_int, _i32p, _i32p, _f32p]
+        L.oracle_bcsr_sgemm.argtypes = [C.c_int, _f32p, C.c_int, C.c_int, C.c_int, _i32p, _i32p, _f32p, _f32p,
+                                        C.c_float, _f32p, C.c_int, C.c_int, C.c_int]
 
     # -- generators -------------------------------------------------------
     def uniform(self, shape, seed: int) -> np.ndarray:
@@ -207,6 +253,32 @@ class Oracle:
     def omp_max_threads(self) -> int:
         return int(self.lib.oracle_omp_max_threads())
 
+    # -- BCSR (oracle/bcsr_oracle.c) -------------------------------------------
+    def bcsr_from_dense(self, dense: np.ndarray, r: int, c: int) -> BCSR:
+        """bcsr.c:19-139."""
+        dense = np.ascontiguousarray(dense, dtype=np.float32)
+        rows, cols = dense.shape
+        k, ne = C.c_int(), C.c_int()
+        self.lib.oracle_bcsr_count(_nz(dense.reshape(-1)), rows, cols, r, c, C.byref(k), C.byref(ne))
+        br, bc = rows // r, cols // c
+        rs = np.empty(br + 1, np.int32)
+        ci = np.empty(max(k.value, 1), np.int32)
+        vals = np.empty(max(k.value * r * c, 1), np.float32)
+        self.lib.oracle_bcsr_fill(_nz(dense.reshape(-1)), rows, cols, r, c, rs, ci, vals)
+        return BCSR(r, c, br, bc, rs, ci[: k.value].copy(), vals[: k.value * r * c].copy())
+
+    def bcsr_sgemm(self, variant: str, X: np.ndarray, W: BCSR, B: np.ndarray, a: float = 0.2,
+                   N: int | None = None) -> np.ndarray:
+        """bcsr_sgemm_<variant> (bcsr.c:141-385); N defaults to len(B)."""
+        X = np.ascontiguousarray(X, dtype=np.float32)
+        M, K = X.shape
+        B = np.ascontiguousarray(B, np.float32).reshape(-1)
+        N = B.size if N is None else N
+        Y = np.empty((M, N), np.float32)
+        self.lib.oracle_bcsr_sgemm(BCSR_VARIANTS.index(variant), _nz(X.reshape(-1)), W.r, W.c, W.br, W.b_row_start,
+                                   _nz(W.b_col_idx), _nz(W.b_values), _nz(B), a, _nz(Y.reshape(-1)), M, N, K)
+        return Y
+
 
 class Reference:
     """The reference's own code (compiled from /root/reference)."""
@@ -226,6 +298,10 @@ class Reference:
         L.ref_sparse_gemm.argtypes = [_f32p, _i32p, _i32p, _i32p, _i32p, _f32p, _f32p, C.c_int, C.c_int,
                                       C.c_int, C.c_int, C.c_float]
         L.ref_gemm_prelu.argtypes = [_f32p, _f32p, _f32p, _f32p, C.c_int, C.c_int, C.c_int, C.c_float]
+        L.ref_bcsr_from_dense.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.c_int, _i32p, _i32p, _f32p,
+                                          C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int]
+        L.ref_bcsr_sgemm.argtypes = [C.c_int, _f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _i32p, _i32p,
+                                     _f32p, _f32p, C.c_float, _f32p, C.c_int, C.c_int, C.c_int]
 
     def tcsc_from_dense(self, dense: np.ndarray) -> TCSC:
         dense = np.ascontiguousarray(dense, np.float32)
@@ -289,6 +365,35 @@ class Reference:
                                  _nz(W.row_index_pos.copy()), _nz(W.row_index_neg.copy()),
                                  _nz(np.ascontiguousarray(B, np.float32).copy()), _nz(Y.reshape(-1)),
                                  M, W.cols, K, int(prelu), a)
+        return Y
+
+
+    def bcsr_from_dense(self, dense: np.ndarray, r: int, c: int):
+        """Returns (BCSR, written): `written` = entries of b_row_start the
+        reference itself writes (the rest are set to k)."""
+        dense = np.ascontiguousarray(dense, np.float32)
+        rows, cols = dense.shape
+        k, w = C.c_int(), C.c_int()
+        d = np.zeros(1, np.int32)
+        self.lib.ref_bcsr_from_dense(_nz(dense.reshape(-1)), rows, cols, r, c, d, d, np.zeros(1, np.float32),
+                                     C.byref(k), C.byref(w), 1)
+        br, bc = rows // r, cols // c
+        rs = np.empty(br + 1, np.int32)
+        ci = np.empty(max(k.value, 1), np.int32)
+        vals = np.empty(max(k.value * r * c, 1), np.float32)
+        self.lib.ref_bcsr_from_dense(_nz(dense.reshape(-1)), rows, cols, r, c, rs, ci, vals, C.byref(k),
+                                     C.byref(w), 0)
+        return BCSR(r, c, br, bc, rs, ci[: k.value].copy(), vals[: k.value * r * c].copy()), w.value
+
+    def bcsr_sgemm(self, variant: str, X, W: BCSR, B, a: float = 0.2, N: int | None = None) -> np.ndarray:
+        X = np.ascontiguousarray(X, np.float32)
+        M, K = X.shape
+        B = np.ascontiguousarray(B, np.float32).reshape(-1)
+        N = B.size if N is None else N
+        Y = np.empty((M, N), np.float32)
+        self.lib.ref_bcsr_sgemm(BCSR_VARIANTS.index(variant), _nz(X.reshape(-1).copy()), W.r, W.c, W.br, W.bc, W.k,
+                                W.b_row_start.copy(), _nz(W.b_col_idx.copy()), _nz(W.b_values.copy()), _nz(B.copy()),
+                                a, _nz(Y.reshape(-1)), M, N, K)
         return Y
 
 

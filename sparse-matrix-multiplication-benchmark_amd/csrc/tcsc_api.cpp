@@ -685,6 +685,12 @@ void host_sgemm(int variant, const float* X, const tcsc_t* W, const float* B, fl
 
 }  // namespace
 
+namespace tcsc {
+void set_error_msg(const char* msg) { g_last_error = msg ? msg : ""; }
+const char* error_msg() { return g_last_error.c_str(); }
+void report_status(int rc) { report(rc); }
+}  // namespace tcsc
+
 extern "C" {
 
 void tcsc_gpu_cache_clear(void) {

@@ -11,6 +11,7 @@
 // prototypes: tcsc_t is a typedef'd anonymous struct, so it mangles as
 // "6tcsc_t"; dense_t is float*.
 #include "../../include/dense/dense.h"
+#include "../../include/sparse/bcsr.h"
 #include "../../include/sparse/tcsc.h"
 
 #define TCSC_EXPORT __attribute__((visibility("default")))
@@ -76,4 +77,42 @@ TCSC_EXPORT void cxx_gemm_prelu_basic(float* X, float* W, float* B, float a, flo
     "_Z16gemm_prelu_basicPfS_S_fS_iii");
 TCSC_EXPORT void cxx_gemm_prelu_basic(float* X, float* W, float* B, float a, float* Y, int M, int N, int K) {
     gemm_prelu_basic(X, W, B, a, Y, M, N, K);
+}
+
+// BCSR (reference sparse/bcsr.h:14-39): bcsr_t is a typedef'd anonymous
+// struct passed by value ("6bcsr_t"); its top-level const/__restrict do not
+// mangle.  These let the reference's test/test_bcsr.cpp link unchanged.
+TCSC_EXPORT bcsr_t* cxx_bcsr_from_dense(float* d, int rows, int cols, int r, int c) __asm__("_Z15bcsr_from_densePfiiii");
+TCSC_EXPORT bcsr_t* cxx_bcsr_from_dense(float* d, int rows, int cols, int r, int c) {
+    return bcsr_from_dense(d, rows, cols, r, c);
+}
+
+TCSC_EXPORT void cxx_bcsr_sgemm_basic(float* X, bcsr_t W, float* B, float* Y, int M, int N, int K) __asm__(
+    "_Z16bcsr_sgemm_basicPf6bcsr_tS_S_iii");
+TCSC_EXPORT void cxx_bcsr_sgemm_basic(float* X, bcsr_t W, float* B, float* Y, int M, int N, int K) {
+    bcsr_sgemm_basic(X, W, B, Y, M, N, K);
+}
+
+TCSC_EXPORT void cxx_bcsr_sgemm_prelu_basic(float* X, bcsr_t W, float* B, float a, float* Y, int M, int N,
+                                            int K) __asm__("_Z22bcsr_sgemm_prelu_basicPf6bcsr_tS_fS_iii");
+TCSC_EXPORT void cxx_bcsr_sgemm_prelu_basic(float* X, bcsr_t W, float* B, float a, float* Y, int M, int N, int K) {
+    bcsr_sgemm_prelu_basic(X, W, B, a, Y, M, N, K);
+}
+
+TCSC_EXPORT void cxx_bcsr_sgemm_avx(float* X, bcsr_t W, float* B, float* Y, int M, int N, int K) __asm__(
+    "_Z14bcsr_sgemm_avxPf6bcsr_tS_S_iii");
+TCSC_EXPORT void cxx_bcsr_sgemm_avx(float* X, bcsr_t W, float* B, float* Y, int M, int N, int K) {
+    bcsr_sgemm_avx(X, W, B, Y, M, N, K);
+}
+
+TCSC_EXPORT void cxx_bcsr_sgemm_prelu_avx(float* X, bcsr_t W, float* B, float a, float* Y, int M, int N,
+                                          int K) __asm__("_Z20bcsr_sgemm_prelu_avxPf6bcsr_tS_fS_iii");
+TCSC_EXPORT void cxx_bcsr_sgemm_prelu_avx(float* X, bcsr_t W, float* B, float a, float* Y, int M, int N, int K) {
+    bcsr_sgemm_prelu_avx(X, W, B, a, Y, M, N, K);
+}
+
+TCSC_EXPORT void cxx_bcsr_sgemm_avx2(float* X, bcsr_t W, float* B, float* Y, int M, int N, int K) __asm__(
+    "_Z15bcsr_sgemm_avx2Pf6bcsr_tS_S_iii");
+TCSC_EXPORT void cxx_bcsr_sgemm_avx2(float* X, bcsr_t W, float* B, float* Y, int M, int N, int K) {
+    bcsr_sgemm_avx2(X, W, B, Y, M, N, K);
 }

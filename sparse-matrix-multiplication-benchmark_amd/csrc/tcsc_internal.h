@@ -126,5 +126,31 @@ hipError_t dense_to_tcsc_fill(const float* D, int rows, int cols, const int* csp
 // Y[m, n] = act(Y[m, n] + B[n]) in place (the dense baseline's epilogue)
 hipError_t launch_bias_act(float* Y, int M, int N, int ldy, const float* B, bool prelu, float a, hipStream_t st);
 hipError_t exclusive_scan_i32(const int* in, int* out, int n, void* tmp, size_t tmp_bytes, hipStream_t st);
+// X (M x K) -> XT (K x ldxt), rows m >= M zero; ldxt = ldxt_for(M) (M rounded up to kTM)
+int ldxt_for(int M);
+hipError_t launch_transpose(const float* X, int M, int K, float* XT, int ldxt, hipStream_t st);
+
+// Error channel shared by every entry point of the library (tcsc_api.cpp):
+// the message behind tcsc_gpu_last_error(), and the host API's policy
+// (stderr + abort unless TCSC_ON_ERROR=continue).
+void set_error_msg(const char* msg);
+const char* error_msg();
+void report_status(int rc);
+
+// ---- BCSR (bcsr_kernels.hip / bcsr_api.cpp) --------------------------------
+struct BcsrArgs {
+    const float* XT = nullptr;  // K x ldxt (X^T)
+    int ldxt = 0, M = 0, N = 0, ldy = 0;
+    const int* colptr = nullptr;  // nbc + 1
+    const int2* ent = nullptr;    // per block column, per (block, block row): {X row, value offset}
+    const float* vals = nullptr;
+    int r = 1, c = 1, nbc = 0;
+    const float* B = nullptr;
+    float* Y = nullptr;
+    float a = 0.f;
+    bool fma = false;    // fused multiply-add (avx variants, or exact ternary products)
+    bool prelu = false;  // PReLU after every update (bcsr.c:208-209)
+};
+hipError_t launch_bcsr(const BcsrArgs& g, hipStream_t st);
 
 }  // namespace tcsc

@@ -841,4 +841,16 @@ hipError_t exclusive_scan_i32(const int* in, int* out, int n, void* tmp, size_t 
     return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, out, n, st);
 }
 
+int ldxt_for(int M) { return ldxt_of(M); }
+
+hipError_t launch_transpose(const float* X, int M, int K, float* XT, int ldxt, hipStream_t st) {
+    if (M <= 0 || K <= 0) return hipSuccess;
+    const bool vec = (K % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+    if (vec)
+        hipLaunchKernelGGL(k_transpose<true>, dim3((K + 63) / 64, ldxt / 64), dim3(256), 0, st, X, M, K, XT, ldxt);
+    else
+        hipLaunchKernelGGL(k_transpose<false>, dim3((K + 63) / 64, ldxt / 64), dim3(256), 0, st, X, M, K, XT, ldxt);
+    return hipGetLastError();
+}
+
 }  // namespace tcsc

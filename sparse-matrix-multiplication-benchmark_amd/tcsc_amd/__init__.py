@@ -41,6 +41,12 @@ EXPORTED_SYMBOLS = (
     "tcsc_gpu_plan_reserve", "tcsc_gpu_plan_destroy", "tcsc_gpu_sgemm", "tcsc_gpu_prepare_x",
     "tcsc_gpu_sgemm_prepared", "tcsc_gpu_from_dense", "tcsc_gpu_dense_sgemm", "tcsc_gpu_last_error",
     "tcsc_gpu_cache_clear", "tcsc_gpu_num_shards", "tcsc_gpu_set_num_shards",
+    # include/sparse/bcsr.h
+    "bcsr_from_dense", "bcsr_sgemm_basic", "bcsr_sgemm_prelu_basic", "bcsr_sgemm_avx", "bcsr_sgemm_prelu_avx",
+    "bcsr_sgemm_avx2", "bcsr_free",
+    # include/bcsr_gpu.h
+    "bcsr_gpu_plan_create", "bcsr_gpu_plan_stats", "bcsr_gpu_plan_reserve", "bcsr_gpu_plan_destroy",
+    "bcsr_gpu_sgemm", "bcsr_gpu_prepare_x", "bcsr_gpu_sgemm_prepared",
 )
 
 
@@ -116,6 +122,9 @@ def lib():
     L.tcsc_gpu_set_num_shards.argtypes = [i]
     L.tcsc_gpu_set_num_shards.restype = None
     L.tcsc_gpu_cache_clear.restype = None
+    from . import bcsr as _bcsr
+
+    _bcsr.bind(L)
     _lib = L
     return L
 

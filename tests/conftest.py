@@ -34,6 +34,26 @@ GOLDEN_NAMES = sorted(
 )
 
 
+BCSR_GOLDEN = os.path.join(GOLDEN, "bcsr")
+BCSR_GOLDEN_NAMES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(BCSR_GOLDEN, "*.npz")))
+
+
+def load_bcsr_golden(name):
+    z = np.load(os.path.join(BCSR_GOLDEN, name + ".npz"), allow_pickle=False)
+    d = {k: z[k] for k in z.files}
+    d["meta"] = json.loads(bytes(d["meta"]).decode())
+    return d
+
+
+def bcsr_of(g):
+    """The reference's bcsr_from_dense output stored in a BCSR fixture."""
+    import pyoracle
+
+    K, N = g["Wd"].shape
+    r, c = int(g["r"]), int(g["c"])
+    return pyoracle.BCSR(r, c, K // r, N // c, g["rs"], g["ci"], g["vals"])
+
+
 @pytest.fixture(scope="session")
 def oracle():
     import pyoracle

@@ -21,7 +21,8 @@ def built_lib():
 
 def declared_functions():
     names = set()
-    for h in ("include/sparse/tcsc.h", "include/dense/dense.h", "include/tcsc_gpu.h"):
+    for h in ("include/sparse/tcsc.h", "include/dense/dense.h", "include/tcsc_gpu.h", "include/sparse/bcsr.h",
+              "include/bcsr_gpu.h"):
         src = open(os.path.join(ROOT, h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         src = re.sub(r"//[^\n]*", "", src)
@@ -54,14 +55,20 @@ def test_reference_signatures_have_c_linkage():
 HEADER_PROBE = r"""
 #include <sparse/tcsc.h>
 #include <tcsc_gpu.h>
+#include <sparse/bcsr.h>
+#include <bcsr_gpu.h>
 typedef void (*gemm_fn)(const dense_t, const tcsc_t *, const dense_t, dense_t, int, int, int);
 typedef void (*prelu_fn)(const dense_t, const tcsc_t *, const dense_t, float, dense_t, int, int, int);
+typedef void (*bgemm_fn)(const dense_t, const bcsr_t, const dense_t, dense_t, int, int, int);
+typedef void (*bprelu_fn)(const dense_t, const bcsr_t, const dense_t, float, dense_t, int, int, int);
 int main(void) {
     gemm_fn g[2] = {tcsc_sgemm_basic, tcsc_sgemm_optimized};
     prelu_fn p[3] = {tcsc_sgemm_prelu_basic, tcsc_sgemm_prelu_optimized_separate,
                      tcsc_sgemm_prelu_optimized_onthego};
+    bgemm_fn bg[3] = {bcsr_sgemm_basic, bcsr_sgemm_avx, bcsr_sgemm_avx2};
+    bprelu_fn bp[2] = {bcsr_sgemm_prelu_basic, bcsr_sgemm_prelu_avx};
     tcsc_gpu_plan_info info;
-    (void)info; (void)g; (void)p;
+    (void)info; (void)g; (void)p; (void)bg; (void)bp;
     return tcsc_gpu_device_count() < 0;
 }
 """
@@ -139,6 +146,13 @@ REFERENCE_MANGLED = {
     "_Z16init_rand_sparseiii": "init_rand_sparse",
     "_Z7comparePfS_ii": "compare",
     "_Z10gemm_basicPfS_S_S_iii": "gemm_basic",
+    # sparse/bcsr.h:14-39 (bcsr_t by value), linked by test/test_bcsr.cpp
+    "_Z15bcsr_from_densePfiiii": "bcsr_from_dense",
+    "_Z16bcsr_sgemm_basicPf6bcsr_tS_S_iii": "bcsr_sgemm_basic",
+    "_Z22bcsr_sgemm_prelu_basicPf6bcsr_tS_fS_iii": "bcsr_sgemm_prelu_basic",
+    "_Z14bcsr_sgemm_avxPf6bcsr_tS_S_iii": "bcsr_sgemm_avx",
+    "_Z20bcsr_sgemm_prelu_avxPf6bcsr_tS_fS_iii": "bcsr_sgemm_prelu_avx",
+    "_Z15bcsr_sgemm_avx2Pf6bcsr_tS_S_iii": "bcsr_sgemm_avx2",
 }
 
 
