@@ -53,6 +53,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-dense-baseline", action="store_true", help="skip the rocBLAS dense comparison (N=1 only)")
+    p.add_argument("--no-bcsr", action="store_true", help="skip the BCSR (1x8 blocks) line (N=1 only)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
     p.add_argument("--override", default="", help="experiments only: e.g. 'K=16448,N=4096' (marks the line)")
     return p.parse_args()
@@ -107,7 +108,8 @@ def main():
     rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
     rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
     tcsc_amd.gpu_from_dense(inp["Wd"], cfg.K, ncols, csp, csn, rip, rin, stream=sh)
-    Wd = inp.pop("Wd") if (world == 1 and not args.no_dense_baseline) else None  # kept for the dense baseline
+    # kept for the dense baseline and the BCSR line
+    Wd = inp.pop("Wd") if (world == 1 and not (args.no_dense_baseline and args.no_bcsr)) else None
     plan = tcsc_amd.Plan.from_device(cfg.K, ncols, csp, csn, rip, rin, 0, ncols, local_rank, sh)
     plan.reserve(cfg.M)
     nnz = npos + nneg
@@ -216,7 +218,7 @@ def main():
                 "valu_add_frac": (adds_per_launch / gather_s) / VALU_ADD_PEAK,
             },
         }
-        if Wd is not None:
+        if Wd is not None and not args.no_dense_baseline:
             # the reference's "TCSC vs Dense" line (main.cpp:379-391) on the
             # device -- gemm_basic's dense product with the same ternary W as an fp32 rocBLAS
             # SGEMM + the bias/PReLU epilogue, same X, B and Y, timed with HIP events
@@ -234,12 +236,44 @@ def main():
                 "tcsc_speedup": dense_s / (elapsed_max / args.steps),
             }
             del Yd
+        if Wd is not None and not args.no_bcsr:
+            out["bcsr"] = bcsr_line(cfg, Wd, X, B, Y, nnz, gather_s, timed, sh, nsplit)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, cfg, variant, X, B, csp, csn, rip[:npos], rin[:nneg])
         print(json.dumps(out), flush=True)
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def bcsr_line(cfg, Wd, X, B, Y, nnz, tcsc_s, timed, sh, n):
+    """the same W as 1x8 BCSR (the block shape of the
+    reference's test/test_bcsr.cpp and of its AVX kernels), k_bcsr timed on
+    the staged X^T like k_stream.  Work: every stored value (zeros inside
+    stored blocks included) is one update per row, M*k*8; its roof is the
+    VALU (one FMA per update for basic; PReLU after every update, bcsr.c:209,
+    adds a multiply, a compare and a select)."""
+    from tcsc_amd import bcsr
+
+    t0 = time.perf_counter()
+    W = bcsr.BcsrMatrix.from_dense(Wd.cpu().numpy(), 1, 8)
+    build_s = time.perf_counter() - t0
+    plan = bcsr.BcsrPlan(W, X.device.index or 0, sh)
+    plan.reserve(cfg.M, cfg.K)
+    plan.prepare_x(X, cfg.M, cfg.K, sh)
+    res = {"kernel": "k_bcsr", "block": "1x8", "blocks": W.k, "stored_values": W.k * 8,
+           "host_bcsr_from_dense_s": build_s}
+    updates = cfg.M * W.k * 8
+    N = Wd.shape[1]
+    for v in ("basic", "prelu_basic"):
+        plan.sgemm_prepared(B, Y, cfg.M, N, cfg.K, N, v, 0.2, sh)
+        t = timed(lambda: plan.sgemm_prepared(B, Y, cfg.M, N, cfg.K, N, v, 0.2, sh), n)
+        res[v] = {"ms": t * 1e3, "g_updates_per_s": updates / t / 1e9, "valu_fma_frac": updates / t / VALU_ADD_PEAK,
+                  "effective_g_add_ops_per_s": (cfg.M * nnz + cfg.M * N) / t / 1e9,
+                  "ms_vs_tcsc_k_stream": t / tcsc_s}
+    plan.destroy()
+    W.free()
+    return res
 
 
 def cpu_baseline(args, cfg, variant, X, B, csp, csn, rip, rin):

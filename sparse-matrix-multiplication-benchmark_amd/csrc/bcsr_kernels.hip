@@ -71,17 +71,22 @@ __device__ __forceinline__ float bcsr_update(float y, float x, float w) {
 
 // (v > 0) ? v : a*v after every update (bcsr.c:209; the avx form's
 // _CMP_GT_OS mask + blend, bcsr.c:302-304, is the same predicate: NaN takes
-// the a*v branch).
-template <bool PRELU>
+// the a*v branch).  PR = 1: that select.  PR = 2, only for 0 < a <= 1:
+// max(v, a*v), the same value for every v (v > 0: a*v <= v; v < 0 and
+// -inf: a*v >= v; +-0: a*v = v; NaN: NaN) in two packed VALU ops per row
+// pair instead of a multiply, a compare and a select per row.
+template <int PR>
 __device__ __forceinline__ float bcsr_act(float v, float a) {
-    if constexpr (PRELU) {
+    if constexpr (PR == 1) {
         return (v > 0.0f) ? v : a * v;
+    } else if constexpr (PR == 2) {
+        return __builtin_fmaxf(v, a * v);
     } else {
         return v;
     }
 }
 
-template <bool FMA, bool PRELU, bool FULL>
+template <bool FMA, int PRELU, bool FULL>
 __global__ void __launch_bounds__(kBcsrWaves * 64)
 k_bcsr(const float* __restrict__ XT, int ldxt, int M, const int* __restrict__ colptr, const int2* __restrict__ ent,
        const float* __restrict__ vals, int c, int nbc, int spb, int nstrips, int N,
@@ -187,7 +192,7 @@ k_bcsr(const float* __restrict__ XT, int ldxt, int M, const int* __restrict__ co
     }
 }
 
-template <bool FMA, bool PRELU, bool FULL>
+template <bool FMA, int PRELU, bool FULL>
 hipError_t launch_v(const BcsrArgs& g, int spb, int nstrips, int vec, hipStream_t st) {
     const dim3 grid((nstrips + kBcsrWaves - 1) / kBcsrWaves, (g.M + kBcsrRows - 1) / kBcsrRows);
     hipLaunchKernelGGL((k_bcsr<FMA, PRELU, FULL>), grid, dim3(kBcsrWaves * 64), 0, st, g.XT, g.ldxt, g.M, g.colptr,
@@ -195,7 +200,7 @@ hipError_t launch_v(const BcsrArgs& g, int spb, int nstrips, int vec, hipStream_
     return hipGetLastError();
 }
 
-template <bool FMA, bool PRELU>
+template <bool FMA, int PRELU>
 hipError_t launch_f(const BcsrArgs& g, int spb, int nstrips, int vec, hipStream_t st) {
     if (g.c % kStrip == 0) return launch_v<FMA, PRELU, true>(g, spb, nstrips, vec, st);
     return launch_v<FMA, PRELU, false>(g, spb, nstrips, vec, st);
@@ -214,8 +219,13 @@ hipError_t launch_bcsr(const BcsrArgs& g, hipStream_t st) {
     if (nstrips > 0x7fffffffLL || (g.M + kBcsrRows - 1) / kBcsrRows > 65535) return hipErrorInvalidValue;
     const int vec = (g.c % 4 == 0) && (g.ldy % 4 == 0) && ((reinterpret_cast<uintptr_t>(g.Y) & 15) == 0);
     const int ns = (int)nstrips;
-    if (g.fma) return g.prelu ? launch_f<true, true>(g, spb, ns, vec, st) : launch_f<true, false>(g, spb, ns, vec, st);
-    return g.prelu ? launch_f<false, true>(g, spb, ns, vec, st) : launch_f<false, false>(g, spb, ns, vec, st);
+    const int pr = !g.prelu ? 0 : (g.a > 0.f && g.a <= 1.f) ? 2 : 1;
+    if (g.fma) {
+        if (pr == 2) return launch_f<true, 2>(g, spb, ns, vec, st);
+        return pr ? launch_f<true, 1>(g, spb, ns, vec, st) : launch_f<true, 0>(g, spb, ns, vec, st);
+    }
+    if (pr == 2) return launch_f<false, 2>(g, spb, ns, vec, st);
+    return pr ? launch_f<false, 1>(g, spb, ns, vec, st) : launch_f<false, 0>(g, spb, ns, vec, st);
 }
 
 }  // namespace tcsc

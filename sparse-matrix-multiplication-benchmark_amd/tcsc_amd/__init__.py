@@ -90,6 +90,16 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise TcscError(f"{LIB_PATH} missing: build it with `make -C {PKG_DIR}`")
+    # One HIP runtime per process: torch ships its own libamdhip64 (SONAME
+    # libamdhip64.so.7, the one the library needs too).  Loaded first, it is
+    # the one the library binds to; loaded after the library's
+    # /opt/rocm copy, torch sees two runtimes and reports no device
+    # (torch.cuda.is_available() False).  So bring torch in first when it is
+    # installed; the library itself never calls into torch.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, i, f = C.c_void_p, C.c_int, C.c_float
     P = C.POINTER(tcsc_t)

@@ -124,11 +124,14 @@ def test_shape_rules_fail_loudly(gpu, monkeypatch):
     W8.free()
 
 
-def test_bcsr_1x8_equals_tcsc_basic(gpu, torch_cuda, oracle):
+def test_bcsr_1x8_equals_tcsc_basic(gpu, torch_cuda, oracle, monkeypatch):
     """Ternary W with 1x8 blocks: bcsr_sgemm_basic adds bias first, then
     X[m,k]*w for every k of a stored block in ascending k -- zeros add +-0,
     an exact no-op here -- which is the TCSC kernel's basic order (bias
-    first, +1/-1 merged in ascending k).  Bit-identical outputs."""
+    first, +1/-1 merged in ascending k) when K is not split over workgroups
+    (TCSC_SLICES=1; this grid is small enough for the cost model to split
+    it).  Bit-identical outputs."""
+    monkeypatch.setenv("TCSC_SLICES", "1")
     torch = torch_cuda
     dev = torch.device("cuda:0")
     M, K, N = 700, 2048, 1032
@@ -151,10 +154,11 @@ def test_bcsr_1x8_equals_tcsc_basic(gpu, torch_cuda, oracle):
     pt.destroy()
 
 
-def test_baseline_cfg4_shape_1x8(gpu, torch_cuda, oracle):
+def test_baseline_cfg4_shape_1x8(gpu, torch_cuda, oracle, monkeypatch):
     """BASELINE cfg4 (M=4096, K=N=16384, 98 % ternary) as 1x8 BCSR: whole
     output bit-identical to the TCSC kernel's basic result, sampled rows
     bit-identical to the oracle (bcsr_sgemm_basic and prelu_basic order)."""
+    monkeypatch.setenv("TCSC_SLICES", "1")
     torch = torch_cuda
     cfg = workloads.CONFIGS[4]
     dev = torch.device("cuda:0")
