@@ -20,7 +20,7 @@
 //    ternary and 98 % sparse at the headline size.
 //  * W is re-laid out once per tcsc_t (the "plan"): for every (K chunk,
 //    wave-column group) one flat stream of 8-byte entries {+-1.0f,
-//    lds_row<<10 | 4*slot}, padded to a multiple of 8.  A wave reads its
+//    lds_row<<10 | 4*slot}, unpadded.  A wave reads its
 //    stream with s_load_dwordx16 (8 entries per scalar load) and selects the
 //    accumulator of the entry's column with s_set_gpr_idx_on (relative VGPR
 //    addressing on the v_pk_fma DST/SRC2): no per-column loop, no branch per
@@ -41,6 +41,24 @@
 namespace tcsc {
 
 typedef float f32x32 __attribute__((ext_vector_type(32)));
+
+// The generated gather loop (tools/gen_gather_asm.py) and its geometry.
+#ifdef TCSC_GATHER_INC
+#include TCSC_GATHER_INC
+#else
+#include "gather_asm.inc"
+#endif
+static_assert(TCSC_GEN_CW == kCW && TCSC_GEN_BATCH == kBatch, "generated loop geometry");
+static_assert(TCSC_GEN_CAP <= kEntGuard, "stream prefetch stays inside the entry guard");
+static_assert(TCSC_GEN_BUDGET == (512 / kWavesPerSimd) / 8 * 8, "generated loop VGPR budget");
+#ifndef TCSC_GEN_TAIL
+#define TCSC_GEN_TAIL 0
+#endif
+// Stream padding.  The generated loop ends every stream with a tail that
+// gathers only its last, partial batch, so streams are unpadded (kPad 1); a
+// loop without the tail needs every (chunk, wave) stream padded to whole
+// batches with no-op entries (+1 x the -0.0 row).
+constexpr int kPad = TCSC_GEN_TAIL ? 1 : kBatch;
 
 // ---------------------------------------------------------------------------
 // Plan building
@@ -79,7 +97,7 @@ __global__ void k_chunk_counts(const int* __restrict__ lbp, const int* __restric
         cnt[i] = (lbp[i + ncols] - lbp[i]) + (lbn[i + ncols] - lbn[i]);
 }
 
-// gcnt[c*G + g] = entries of group g in chunk c, rounded up to kBatch.
+// gcnt[c*G + g] = entries of group g in chunk c, rounded up to kPad.
 __global__ void k_group_counts(const int* __restrict__ cptr, int ncols, int nch, int G, int* __restrict__ gcnt) {
     const long long total = (long long)nch * G;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -87,7 +105,7 @@ __global__ void k_group_counts(const int* __restrict__ cptr, int ncols, int nch,
         const int c = (int)(i / G), g = (int)(i % G);
         const int n0 = g * kCW, n1 = min(n0 + kCW, ncols);
         const int real = cptr[(long long)c * ncols + n1] - cptr[(long long)c * ncols + n0];
-        gcnt[i] = (real + kBatch - 1) / kBatch * kBatch;
+        gcnt[i] = (real + kPad - 1) / kPad * kPad;
     }
 }
 
@@ -193,27 +211,11 @@ __global__ void __launch_bounds__(256) k_transpose(const float* __restrict__ X, 
     }
 }
 
-#ifdef TCSC_GATHER_INC
-#include TCSC_GATHER_INC
-#else
-#include "gather_asm.inc"
-#endif
-static_assert(TCSC_GEN_CW == kCW && TCSC_GEN_BATCH == kBatch, "generated loop geometry");
-static_assert(TCSC_GEN_CAP <= kEntGuard, "stream prefetch stays inside the entry guard");
-static_assert(TCSC_GEN_BUDGET == (512 / kWavesPerSimd) / 8 * 8, "generated loop VGPR budget");
-
-// Consume this wave's stream for one chunk: `nb` batches of 8 entries at
-// `stream` (entries padded to a multiple of 8).  The chunk's first 64-entry
-// block (lane i = entry i) is already in the PAR pair (v232/v233 for even
-// chunks, v238/v239 for odd ones); the asm starts by loading the next
-// chunk's first block (at `next`) into the other pair, so that load has a
-// whole chunk to land.  The schedule and register map are in
-// tools/gen_gather_asm.py.  s_set_gpr_idx_* writes M0, which the compiler
-// also uses (LDS-DMA destination): the asm saves it in s68 and restores it.
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(4))) const i32x16 const_i32x16;
 
-// Consume this wave's stream for one chunk: `nb` batches of kBatch entries.
+// Consume this wave's stream for one chunk: `nb` whole batches of kBatch
+// entries, then `rem` more (the tail; TCSC_GEN_TAIL).
 // The first TCSC_GEN_CAP entries are already in the pinned SGPR buffer `sb`
 // (loaded by the caller's scalar loads); `ptr` is the stream's address, used
 // to reload the buffer for streams longer than the capacity.  The schedule
@@ -222,13 +224,13 @@ typedef __attribute__((address_space(4))) const i32x16 const_i32x16;
 // touched at the start (loads into the pinned `junk` SGPR, never read), so
 // the real s_load after this gather hits in K$.  Whoever runs after the loop
 // must wait lgkmcnt(0) before the junk register is released.
-__device__ __forceinline__ void gather_stream(unsigned nb, i32x16 (&sb)[TCSC_SBUF_VECS], unsigned long long ptr,
+__device__ __forceinline__ void gather_stream(unsigned nb, unsigned rem, i32x16 (&sb)[TCSC_SBUF_VECS], unsigned long long ptr,
                                               const void* tptr, int& junk, unsigned lane, unsigned mask,
                                               f32x32 (&acc)[TCSC_ACC_VECS]) {
     asm volatile(TCSC_GATHER_ASM
                  : [nb] "+s"(nb), TCSC_ACC_OPERANDS(acc), TCSC_SBUF_OPERANDS(sb), TCSC_PTR_OPERAND(ptr),
                    TCSC_JUNK_OPERAND(junk)
-                 : [lane] "v"(lane * 16u), [mask] "v"(mask), [tptr] "s"(tptr)
+                 : [lane] "v"(lane * 16u), [mask] "v"(mask), [tptr] "s"(tptr), [rem] "s"(rem)
                  : TCSC_GATHER_CLOBBERS);
 }
 
@@ -259,15 +261,64 @@ struct DmaState {
     size_t chunk_bytes;            // kTK * ldxt * 4
 };
 
+#ifndef TCSC_DMA_OFFSET
+#define TCSC_DMA_OFFSET 1
+#endif
+// TCSC_DMA_OFFSET: one M0 write per group of up to 4 rows.  The instruction
+// offset (13-bit signed, 0..3 KiB here) moves the LDS destination (M0 +
+// offset + 16*lane) and the global source alike; voff[i] carries
+// -(i % 4) KiB to cancel it on the global side: 3 instructions per row ->
+// ~1.7 (A/B: -0.9 % k_stream at cfg4).  0 = one M0 write per row.
+template <int N>
+__device__ __forceinline__ void dma_rows(unsigned m0, const unsigned* v, const char* src) {
+    if constexpr (N == 4)
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %5\n\t"
+                     "global_load_lds_dwordx4 %2, %5 offset:1024\n\tglobal_load_lds_dwordx4 %3, %5 offset:2048\n\t"
+                     "global_load_lds_dwordx4 %4, %5 offset:3072"
+                     :
+                     : "s"(m0), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "s"(src)
+                     : "memory");
+    else if constexpr (N == 3)
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %4\n\t"
+                     "global_load_lds_dwordx4 %2, %4 offset:1024\n\tglobal_load_lds_dwordx4 %3, %4 offset:2048"
+                     :
+                     : "s"(m0), "v"(v[0]), "v"(v[1]), "v"(v[2]), "s"(src)
+                     : "memory");
+    else if constexpr (N == 2)
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\t"
+                     "global_load_lds_dwordx4 %2, %3 offset:1024"
+                     :
+                     : "s"(m0), "v"(v[0]), "v"(v[1]), "s"(src)
+                     : "memory");
+    else
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+                     :
+                     : "s"(m0), "v"(v[0]), "s"(src)
+                     : "memory");
+}
+
+template <int I0>
+__device__ __forceinline__ void dma_groups(const DmaState& d, unsigned m0base) {
+    if constexpr (I0 < kDmaPerWave) {
+        constexpr int n = kDmaPerWave - I0 < 4 ? kDmaPerWave - I0 : 4;
+        dma_rows<n>(m0base + I0 * kRowBytes, d.voff + I0, d.next);
+        dma_groups<I0 + 4>(d, m0base);
+    }
+}
+
 __device__ __forceinline__ void dma_next_chunk(DmaState& d, int buf) {
 #if !((defined(TCSC_ABLATION) && TCSC_ABLATION == 6) || defined(TCSC_NODMA))
     const unsigned m0base = d.lds_wave + (unsigned)(buf * (kBufRows * kRowBytes));
+#if TCSC_DMA_OFFSET
+    dma_groups<0>(d, m0base);
+#else
 #pragma unroll
     for (int i = 0; i < kDmaPerWave; ++i)
         asm volatile("s_add_u32 m0, %0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3"
                      :
                      : "s"(m0base), "n"(i * kRowBytes), "v"(d.voff[i]), "s"(d.next)
                      : "memory", "scc");
+#endif
 #endif
     d.next += d.chunk_bytes;
 }
@@ -353,7 +404,8 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         dma.next = reinterpret_cast<const char*>(XT + (size_t)c_begin * kTK * ldxt + m0);
 #pragma unroll
         for (int i = 0; i < kDmaPerWave; ++i)
-            dma.voff[i] = 16u * lane + (unsigned)((wave * kDmaPerWave + i) * ldxt * 4);
+            dma.voff[i] = 16u * lane + (unsigned)((wave * kDmaPerWave + i) * ldxt * 4) -
+                          (TCSC_DMA_OFFSET ? (unsigned)((i % 4) * kRowBytes) : 0u);
         dma.lds_wave = (unsigned)reinterpret_cast<uintptr_t>(lds) + (unsigned)(wave * kDmaPerWave * kRowBytes);
         const bool dma_wave = wave < kDmaWaves;  // uniform
         int buf = c_begin % kNBuf;
@@ -424,7 +476,8 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                 s0n = __builtin_amdgcn_readlane(vs0, idx);
                 s1n = __builtin_amdgcn_readlane(vs1, idx);
             }
-            const unsigned nb = active ? (unsigned)(s1 - s0) / kBatch : 0u;
+            const unsigned n_ent = active ? (unsigned)(s1 - s0) : 0u;
+            const unsigned nb = n_ent / kBatch, rem = n_ent % kBatch;  // whole batches, then the tail
 #ifdef TCSC_STAMPS
             const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
             asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[36:51]}"(sb[0]), "+{s[52:67]}"(sb[1]), "+{s[68:83]}"(sb[2]));
@@ -444,7 +497,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
             else if (nb >= (unsigned)TCSC_PRIO) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
 #endif
-            gather_stream(nb, sb, reinterpret_cast<unsigned long long>(ent + s0), ent + s0n, junk, lane, mask, acc);
+            gather_stream(nb, rem, sb, reinterpret_cast<unsigned long long>(ent + s0), ent + s0n, junk, lane, mask, acc);
 #ifdef TCSC_STAMPS
             st_gather += __builtin_amdgcn_s_memtime() - ts1;
 #endif

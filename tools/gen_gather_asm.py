@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Generate the gather loop of kernel K1 (k_stream) for one register geometry.
 
-    gen_gather_asm.py [--cw 16] [--batch 4] [--cap 24] [--budget 128] [--depth 1] [-o path]
+    gen_gather_asm.py [--cw 16] [--batch 4] [--cap 24] [--budget 128] [--depth 1] [--tail 1] [-o path]
 
 Why generated: the loop is a fully unrolled, software-pipelined sequence of
 positions whose register names are static per position; writing it by hand
@@ -28,6 +28,18 @@ Position p does ISSUE(p) then FMA(p-DEPTH), so a batch's LDS latency hides
 under the FMAs of the DEPTH batches before it (DEPTH*BATCH reads stay in
 flight).  X quads cycle through DEPTH+1 register sets.
 
+Stream lengths (--tail):
+  1 (default) unpadded streams: %[nb] = whole batches, %[rem] = entries of
+    the last, partial batch.  Position p first checks whether the whole
+    batches are used up and, if so, jumps to tail p, which issues only the
+    rem reads of batch p, finishes batch p-1 and FMAs the rem entries
+    (generate_tail).  At 98 % sparsity a wave's chunk stream averages ~15
+    entries, so padding to whole batches cost ~10 % of the gathers.
+  0 the plan pads every stream to a multiple of BATCH with no-op entries
+    (+1 x the -0.0 row) and the loop runs whole batches (generate).
+tests/test_gather_gen.py runs the generated instruction lists through a
+small interpreter for every stream length.
+
 TCSC_ABLATION = 1..5 selects timing-only variants (wrong results):
 1 no index mode, 3 no LDS read, 4 no FMA, 5 no gather.
 """
@@ -37,11 +49,12 @@ import sys
 
 
 class Geo:
-    def __init__(self, cw, batch, cap, budget, depth=1, touch=4):
+    def __init__(self, cw, batch, cap, budget, depth=1, touch=4, tail=1):
         assert cw % 8 == 0 and cap % batch == 0 and 36 + 2 * cap <= 100
         assert 1 <= depth and depth * batch <= 15, "lgkmcnt counts to 15"
         self.cw, self.batch, self.cap, self.budget, self.depth = cw, batch, cap, budget, depth
         self.touch = touch  # scalar-cache lines of the NEXT chunk's stream touched at the start
+        self.tail = bool(tail)
         self.npos = cap // batch
         assert self.npos > depth
         nacc, self.nx = 4 * cw, 4 * batch * (depth + 1)
@@ -61,23 +74,27 @@ def sreg(g, j, w):
     return g.sbase + 2 * j + w
 
 
-def issue(g, p):
+def issue(g, p, n=None):
+    """Reads of batch p's first n entries (default: the whole batch)."""
+    n = g.batch if n is None else n
     x = g.xset[p % (g.depth + 1)]
     out = []
-    for i in range(g.batch):
+    for i in range(n):
         out.append(f"v_bfi_b32 v{x + 4 * i}, %[mask], %[lane], s{sreg(g, g.batch * p + i, 1)}")
     if ABL != 3:
-        for i in range(g.batch):
+        for i in range(n):
             out.append(f"ds_read_b128 v[{x + 4 * i}:{x + 4 * i + 3}], v{x + 4 * i}")
     return out
 
 
-def fma(g, p, wait):
+def fma(g, p, wait, n=None):
+    """FMAs of batch p's first n entries after waiting for all but `wait` LDS reads."""
+    n = g.batch if n is None else n
     x = g.xset[p % (g.depth + 1)]
     out = [f"s_waitcnt lgkmcnt({wait})"]
     if ABL == 4:
         return out
-    for i in range(g.batch):
+    for i in range(n):
         j = g.batch * p + i
         w1, sg = sreg(g, j, 1), sreg(g, j, 0)
         pair = f"s[{sg}:{sg + 1}]"
@@ -157,6 +174,45 @@ def generate(g):
     return L
 
 
+def generate_tail(g):
+    """Unpadded streams: %[nb] whole batches + %[rem] (0 .. BATCH-1) entries.
+    The steady state issues exactly what the padded loop issues (the
+    end-of-stream check moves ahead of ISSUE); only the last batch differs.
+    Tail p: the DEPTH batches before p are issued, not yet FMA'd; it issues
+    the rem reads of batch p, FMAs those batches oldest first, then the rem
+    entries."""
+    if ABL == 5:
+        return []
+    D = g.depth
+    L = ["s_load_dword %[junk], %[tptr], " + hex(min(64 * t, 8 * g.cap - 4)) for t in range(g.touch)]
+    L.append(".Lphase%=:")
+    for p in range(g.npos):
+        L += [f"s_cmp_eq_u32 %[nb], {p}", f"s_cbranch_scc1 .Ltail{p}%="]
+        L += issue(g, p)
+        if p >= D:
+            L += fma(g, p - D, g.batch * D)
+    # a full phase with batches left: finish its last batches, reload, go on
+    for q in range(g.npos - D, g.npos):
+        L += fma(g, q, g.batch * (g.npos - 1 - q))
+    L.append(f"s_sub_u32 %[nb], %[nb], {g.npos}")
+    L += reload(g)
+    L.append("s_branch .Lphase%=")
+    for p in range(g.npos):
+        L.append(f".Ltail{p}%=:")
+        for r in range(g.batch - 1):
+            L += [f"s_cmp_eq_u32 %[rem], {r}", f"s_cbranch_scc1 .Lt{p}r{r}%="]
+        for r in range(g.batch - 1, -1, -1):
+            L.append(f".Lt{p}r{r}%=:")
+            L += issue(g, p, r)
+            for q in range(max(0, p - D), p):
+                L += fma(g, q, g.batch * (p - 1 - q) + r)
+            if r:
+                L += fma(g, p, 0, r)
+            if not (p == g.npos - 1 and r == 0):
+                L.append("s_branch .Lend%=")
+    L.append(".Lend%=:")
+    return L
+
 def emit(f, name, lines):
     f.write(f"#define {name} \\\n")
     for l in lines:
@@ -171,11 +227,13 @@ def write_inc(path, g):
     assert (2 * g.cap) % 16 == 0
     with open(path, "w") as f:
         f.write("// GENERATED by tools/gen_gather_asm.py -- do not edit by hand.\n")
-        f.write(f"// geometry: cw={g.cw} batch={g.batch} cap={g.cap} vgpr budget={g.budget} depth={g.depth}: "
+        f.write(f"// geometry: cw={g.cw} batch={g.batch} cap={g.cap} vgpr budget={g.budget} depth={g.depth} "
+                f"tail={int(g.tail)}: "
                 f"acc v[{g.acc}:{g.acc + 4 * g.cw - 1}], X v[{g.xbase}:{g.xbase + g.nx - 1}], "
                 f"stream s[{g.sbase}:{g.slast}]\n")
         f.write(f"#define TCSC_GEN_CW {g.cw}\n#define TCSC_GEN_BATCH {g.batch}\n#define TCSC_GEN_CAP {g.cap}\n")
         f.write(f"#define TCSC_GEN_BUDGET {g.budget}\n#define TCSC_ACC_VECS {nvec}\n#define TCSC_SBUF_VECS {nsv}\n")
+        f.write(f"#define TCSC_GEN_TAIL {int(g.tail)}\n")
         ops = ", ".join(f'"+{{v[{g.acc + 32 * i}:{g.acc + 32 * i + 31}]}}"(acc[{i}])' for i in range(nvec))
         f.write(f"#define TCSC_ACC_OPERANDS(acc) {ops}\n")
         sops = ", ".join(f'"+{{s[{g.sbase + 16 * i}:{g.sbase + 16 * i + 15}]}}"(sb[{i}])' for i in range(nsv))
@@ -195,7 +253,7 @@ def write_inc(path, g):
             if a:
                 f.write(f"#elif TCSC_ABLATION == {a}\n")
             ABL = a
-            emit(f, "TCSC_GATHER_ASM", generate(g))
+            emit(f, "TCSC_GATHER_ASM", generate_tail(g) if g.tail else generate(g))
         f.write("#else\n#define TCSC_GATHER_ASM \"\"\n#endif\n")
         ABL = 0
 
@@ -208,11 +266,12 @@ def main():
     ap.add_argument("--budget", type=int, default=128)
     ap.add_argument("--depth", type=int, default=1)
     ap.add_argument("--touch", type=int, default=0)
+    ap.add_argument("--tail", type=int, default=1)
     here = os.path.dirname(os.path.abspath(__file__))
     ap.add_argument("-o", default=os.path.join(here, "..", "sparse-matrix-multiplication-benchmark_amd", "csrc",
                                                "gather_asm.inc"))
     a = ap.parse_args()
-    write_inc(a.o, Geo(a.cw, a.batch, a.cap, a.budget, a.depth, a.touch))
+    write_inc(a.o, Geo(a.cw, a.batch, a.cap, a.budget, a.depth, a.touch, a.tail))
     print(a.o)
 
 
