@@ -173,30 +173,45 @@ __global__ void k_fill_pads(const int* __restrict__ cptr, const int* __restrict_
 template <bool VEC>
 __global__ void __launch_bounds__(256) k_transpose(const float* __restrict__ X, int M, int K, float* __restrict__ XT,
                                                    int ldxt) {
-    __shared__ float t[64][65];
-    const int k0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
     if (VEC) {
-        const int q = threadIdx.x & 15, rr = threadIdx.x >> 4;  // 16 float4 per 64-wide row
+        // 64 (m) x 128 (k) tile: 512-B row reads, all 8 float4 loads of a
+        // thread in flight before the first LDS write.  Row stride 129 keeps
+        // the column reads conflict-free (129 = 1 mod 64 banks).
+        __shared__ float tv[64][129];
+        const int k0 = blockIdx.x * 128, m0 = blockIdx.y * 64;
+        const int q2 = threadIdx.x & 31, r2 = threadIdx.x >> 5;  // 32 float4 per 128-wide row
+        float4 v[8];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = rr + 16 * i, m = m0 + r, k = k0 + 4 * q;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (m < M && k < K) v = *reinterpret_cast<const float4*>(X + (size_t)m * K + k);
-            t[r][4 * q + 0] = v.x;
-            t[r][4 * q + 1] = v.y;
-            t[r][4 * q + 2] = v.z;
-            t[r][4 * q + 3] = v.w;
+        for (int i = 0; i < 8; ++i) {
+            const int m = m0 + r2 + 8 * i, k = k0 + 4 * q2;
+            v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (m < M && k < K) {
+                typedef float nt4 __attribute__((ext_vector_type(4)));
+                const nt4 w = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(X + (size_t)m * K + k));
+                v[i] = make_float4(w.x, w.y, w.z, w.w);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int r = r2 + 8 * i;
+            tv[r][4 * q2 + 0] = v[i].x;
+            tv[r][4 * q2 + 1] = v[i].y;
+            tv[r][4 * q2 + 2] = v[i].z;
+            tv[r][4 * q2 + 3] = v[i].w;
         }
         __syncthreads();
+        const int q = threadIdx.x & 15, rr = threadIdx.x >> 4;  // 16 float4 per 64-wide XT row piece
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 8; ++i) {
             const int kk = rr + 16 * i, k = k0 + kk;
             if (k < K)
                 *reinterpret_cast<float4*>(XT + (size_t)k * ldxt + m0 + 4 * q) =
-                    make_float4(t[4 * q + 0][kk], t[4 * q + 1][kk], t[4 * q + 2][kk], t[4 * q + 3][kk]);
+                    make_float4(tv[4 * q + 0][kk], tv[4 * q + 1][kk], tv[4 * q + 2][kk], tv[4 * q + 3][kk]);
         }
         return;
     }
+    __shared__ float t[64][65];
+    const int k0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -855,7 +870,7 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
         const int ldxt = ldxt_of(g.M);
         const bool vec = (g.K % 4 == 0) && ((reinterpret_cast<uintptr_t>(g.X) & 15) == 0);
         if (vec)
-            hipLaunchKernelGGL(k_transpose<true>, dim3((g.K + 63) / 64, ldxt / 64), dim3(256), 0, st, g.X, g.M, g.K,
+            hipLaunchKernelGGL(k_transpose<true>, dim3((g.K + 127) / 128, ldxt / 64), dim3(256), 0, st, g.X, g.M, g.K,
                                g.XT, ldxt);
         else
             hipLaunchKernelGGL(k_transpose<false>, dim3((g.K + 63) / 64, ldxt / 64), dim3(256), 0, st, g.X, g.M,
@@ -900,7 +915,7 @@ hipError_t launch_transpose(const float* X, int M, int K, float* XT, int ldxt, h
     if (M <= 0 || K <= 0) return hipSuccess;
     const bool vec = (K % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
     if (vec)
-        hipLaunchKernelGGL(k_transpose<true>, dim3((K + 63) / 64, ldxt / 64), dim3(256), 0, st, X, M, K, XT, ldxt);
+        hipLaunchKernelGGL(k_transpose<true>, dim3((K + 127) / 128, ldxt / 64), dim3(256), 0, st, X, M, K, XT, ldxt);
     else
         hipLaunchKernelGGL(k_transpose<false>, dim3((K + 63) / 64, ldxt / 64), dim3(256), 0, st, X, M, K, XT, ldxt);
     return hipGetLastError();
