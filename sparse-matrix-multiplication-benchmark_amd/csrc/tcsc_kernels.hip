@@ -638,7 +638,13 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                         dst = ws + ((size_t)t.z * M + row) * ncols + col;
                     }
                     if (vec_ok && col + 3 < ncols) {
-                        *reinterpret_cast<float4*>(dst) = v;
+                        if (OUT == 0) {  // Y is never re-read here: keep it out of L2's way
+                            typedef float nt4 __attribute__((ext_vector_type(4)));
+                            nt4 w = {v.x, v.y, v.z, v.w};
+                            __builtin_nontemporal_store(w, reinterpret_cast<nt4*>(dst));
+                        } else {
+                            *reinterpret_cast<float4*>(dst) = v;
+                        }
                     } else {
                         dst[0] = v.x;
                         if (col + 1 < ncols) dst[1] = v.y;
