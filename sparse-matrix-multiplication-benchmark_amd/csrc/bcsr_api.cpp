@@ -42,6 +42,10 @@ struct bcsr_gpu_plan {
     float* xt = nullptr;   // workspace: X^T
     size_t xt_bytes = 0;
     size_t bytes = 0;
+    // what bcsr_gpu_prepare_x left in xt: (M, K) of the staged X, or -1 when
+    // nothing is staged (never staged, the workspace was reallocated, or a
+    // whole bcsr_gpu_sgemm overwrote it with its own X)
+    int staged_M = -1, staged_K = -1;
 };
 
 namespace {
@@ -189,6 +193,7 @@ int reserve(bcsr_gpu_plan* p, int M, int K) {
         p->xt = nullptr;
         p->xt_bytes = 0;
     }
+    p->staged_M = p->staged_K = -1;
     BCSR_HIP(hipMalloc(&p->xt, want));
     p->xt_bytes = want;
     return TCSC_OK;
@@ -211,12 +216,21 @@ int run(const bcsr_gpu_plan* pc, const float* dX, const float* dB, float* dY, in
     }
     if (M == 0 || (stage != 1 && N == 0)) return TCSC_OK;
     bcsr_gpu_plan* p = const_cast<bcsr_gpu_plan*>(pc);
+    // the gather reads X^T with the pitch of the M it was staged for
+    if (stage == 2 && K > 0 && (p->staged_M != M || p->staged_K != K))
+        return fail(TCSC_E_ARG, "bcsr_gpu_sgemm_prepared: M=%d K=%d but the staged X is %s (bcsr_gpu_prepare_x first)",
+                    M, K, p->staged_M < 0 ? "absent" : "another shape");
     if (K > 0 && (rc = reserve(p, M, K)) != TCSC_OK) return rc;
     DevGuard dg(p->device);
     const int ldxt = tcsc::ldxt_for(M);
     if (stage != 2 && K > 0) {
         if (!dX) return fail(TCSC_E_ARG, "bcsr_gpu_sgemm: NULL X");
+        p->staged_M = p->staged_K = -1;
         BCSR_HIP(tcsc::launch_transpose(dX, M, K, p->xt, ldxt, st));
+        if (stage == 1) {
+            p->staged_M = M;
+            p->staged_K = K;
+        }
     }
     if (stage == 1) return TCSC_OK;
     if (!dB || !dY) return fail(TCSC_E_ARG, "bcsr_gpu_sgemm: NULL B or Y");

@@ -13,7 +13,9 @@
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
 
+#include <algorithm>
 #include <cstdarg>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -36,9 +38,13 @@ struct tcsc_gpu_plan {
     long long n_entries = 0;
     int2* ent = nullptr;   // stream entries (+ guard batch)
     int* sptr = nullptr;   // stream starts, n_chunks*n_groups + 1
-    float* ws = nullptr;   // split-K partial slabs (tcsc_gpu_plan_reserve)
+    float* ws = nullptr;   // X^T + split-K partial slabs (tcsc_gpu_plan_reserve)
     size_t ws_bytes = 0;
     size_t bytes = 0;
+    // M of the X that tcsc_gpu_prepare_x left in ws (X^T's pitch depends on
+    // it), or -1 when nothing is staged: never staged, the workspace was
+    // reallocated, or a whole tcsc_gpu_sgemm overwrote it with its own X
+    int staged_M = -1;
 };
 
 namespace {
@@ -180,6 +186,85 @@ size_t wanted_workspace(const tcsc_gpu_plan* p, int M) {
     return tcsc::xt_bytes(M, p->rows) + tcsc::workspace_bytes(M, p->cols, s);
 }
 
+// The plan build assumes what tcsc_from_dense produces (tcsc.c:48-60): in
+// every column the row indices lie in [0, rows) and ascend.  The reference's
+// loops take any order (tcsc.c:86-93), so a column out of order is sorted in
+// a copy (its sums then run in ascending k: within the float tolerance of
+// the reference's order, exact on integer-valued inputs).  A row outside
+// [0, rows) or a decreasing col_start would make the reference read outside
+// X or the index arrays: TCSC_E_ARG.  Columns [c0, c1) of one sign; on
+// return `sorted` is empty when the slice is already in order, else the
+// whole slice (rebased to cs[c0]) with every column sorted.
+int check_index_host(const int* cs, const int* ri, int c0, int c1, int rows, int n_elem, const char* sign,
+                     std::vector<int>& sorted) {
+    sorted.clear();
+    bool in_order = true;
+    for (int j = c0; j < c1; ++j) {
+        const int a = cs[j], b = cs[j + 1];
+        if (a < 0 || b < a || b > n_elem) {
+            set_error("tcsc_gpu_plan_create: col_start_%s[%d..%d] = %d, %d is not a range inside [0, %d]", sign, j,
+                      j + 1, a, b, n_elem);
+            return TCSC_E_ARG;
+        }
+        for (int i = a; i < b; ++i) {
+            const int k = ri[i];
+            if (k < 0 || k >= rows) {
+                set_error("tcsc_gpu_plan_create: row_index_%s[%d] = %d outside [0, %d) (column %d)", sign, i, k, rows,
+                          j);
+                return TCSC_E_ARG;
+            }
+            if (i > a && k < ri[i - 1]) in_order = false;
+        }
+    }
+    if (in_order) return TCSC_OK;
+    const int base = cs[c0];
+    sorted.assign(ri + base, ri + cs[c1]);
+    for (int j = c0; j < c1; ++j) std::sort(sorted.begin() + (cs[j] - base), sorted.begin() + (cs[j + 1] - base));
+    return TCSC_OK;
+}
+
+// Content fingerprint of index arrays for the host API's plan cache.  The
+// cache is keyed by the tcsc_t pointer, but the reference reads the arrays
+// on every call and keeps no state, so an in-place rebuild with the same
+// counts, or a tcsc_t released with plain free() (as the reference's
+// test_bcsr.cpp does for bcsr_t) whose addresses malloc hands to the next
+// matrix, must not hit a stale plan.  Multilinear hash over 32-bit pairs in
+// four lanes (it vectorises: ~1 ms for cfg4's 21 MB of indices, next to the
+// ~5 ms H2D of X every call pays), position-dependent, murmur-finalised.
+uint64_t fmix64(uint64_t h) {
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+    h *= 0xc4ceb9fe1a85ec53ull;
+    return h ^ (h >> 33);
+}
+
+uint64_t hash_ints(const int* p, long long n, uint64_t h) {
+    h = fmix64(h ^ (uint64_t)n);
+    if (!p || n <= 0) return h;
+    const uint32_t* u = reinterpret_cast<const uint32_t*>(p);
+    static constexpr uint32_t kA[4] = {0x9e3779b9u, 0x85ebca6bu, 0xc2b2ae35u, 0x27d4eb2fu};
+    static constexpr uint32_t kB[4] = {0x165667b1u, 0xd3a2646cu, 0xfd7046c5u, 0xb55a4f09u};
+    uint64_t acc[4] = {0, 0, 0, 0};
+    long long i = 0;
+    for (; i + 8 <= n; i += 8) {
+        const uint32_t pos = (uint32_t)i;
+        for (int j = 0; j < 4; ++j)
+            acc[j] += (uint64_t)(u[i + 2 * j] + kA[j] + pos) * (uint64_t)(u[i + 2 * j + 1] + kB[j]);
+    }
+    for (; i < n; ++i) acc[i & 3] += (uint64_t)(u[i] + kA[i & 3] + (uint32_t)i) * (uint64_t)(kB[i & 3] | 1u);
+    for (int j = 0; j < 4; ++j) h = fmix64(h ^ acc[j]) + (uint64_t)j;
+    return h;
+}
+
+uint64_t tcsc_fingerprint(const tcsc_t* W) {
+    uint64_t h = fmix64(((uint64_t)(uint32_t)W->rows << 32) | (uint32_t)W->cols);
+    h = hash_ints(W->col_start_pos, (long long)W->cols + 1, h);
+    h = hash_ints(W->col_start_neg, (long long)W->cols + 1, h);
+    h = hash_ints(W->row_index_pos, W->n_elem_pos, h);
+    return hash_ints(W->row_index_neg, W->n_elem_neg, h);
+}
+
 class DeviceGuard {
   public:
     explicit DeviceGuard(int dev) {
@@ -222,6 +307,7 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
     g.K = p->rows;
     g.ent = p->ent;
     g.sptr = p->sptr;
+    g.n_entries = p->n_entries;
     g.n_groups = p->n_groups;
     g.ncols = p->cols;
     g.nnz = p->n_pos + p->n_neg;
@@ -261,6 +347,13 @@ int tcsc_gpu_plan_create(const tcsc_t* W, int col_begin, int col_end, int device
     }
     *out = nullptr;
     const int nc = col_end - col_begin;
+    std::vector<int> sorted_p, sorted_n;
+    int rc = check_index_host(W->col_start_pos, W->row_index_pos, col_begin, col_end, W->rows, W->n_elem_pos, "pos",
+                              sorted_p);
+    if (rc == TCSC_OK)
+        rc = check_index_host(W->col_start_neg, W->row_index_neg, col_begin, col_end, W->rows, W->n_elem_neg, "neg",
+                              sorted_n);
+    if (rc != TCSC_OK) return rc;
     DeviceGuard dg(device);
     if (!dg.ok()) {
         set_error("tcsc_gpu_plan_create: cannot select device %d", device);
@@ -269,6 +362,8 @@ int tcsc_gpu_plan_create(const tcsc_t* W, int col_begin, int col_end, int device
     hipStream_t st = static_cast<hipStream_t>(stream);
     const int p0 = W->col_start_pos[col_begin], p1 = W->col_start_pos[col_end];
     const int q0 = W->col_start_neg[col_begin], q1 = W->col_start_neg[col_end];
+    const int* hrip = sorted_p.empty() ? W->row_index_pos + p0 : sorted_p.data();
+    const int* hrin = sorted_n.empty() ? W->row_index_neg + q0 : sorted_n.data();
     // column slice, rebased to 0
     std::vector<int> csp(nc + 1), csn(nc + 1);
     for (int j = 0; j <= nc; ++j) {
@@ -283,12 +378,10 @@ int tcsc_gpu_plan_create(const tcsc_t* W, int col_begin, int col_end, int device
     HIP_TRY(hipMemcpyAsync(dcsp.p, csp.data(), (nc + 1) * sizeof(int), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(dcsn.p, csn.data(), (nc + 1) * sizeof(int), hipMemcpyHostToDevice, st));
     if (p1 > p0)
-        HIP_TRY(hipMemcpyAsync(drip.p, W->row_index_pos + p0, (size_t)(p1 - p0) * sizeof(int),
-                               hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(drip.p, hrip, (size_t)(p1 - p0) * sizeof(int), hipMemcpyHostToDevice, st));
     if (q1 > q0)
-        HIP_TRY(hipMemcpyAsync(drin.p, W->row_index_neg + q0, (size_t)(q1 - q0) * sizeof(int),
-                               hipMemcpyHostToDevice, st));
-    int rc = build_plan(W->rows, 0, nc, p1 - p0, q1 - q0, dcsp.as<int>(), dcsn.as<int>(), drip.as<int>(),
+        HIP_TRY(hipMemcpyAsync(drin.p, hrin, (size_t)(q1 - q0) * sizeof(int), hipMemcpyHostToDevice, st));
+    rc = build_plan(W->rows, 0, nc, p1 - p0, q1 - q0, dcsp.as<int>(), dcsn.as<int>(), drip.as<int>(),
                         drin.as<int>(), device, st, out);
     if (rc == TCSC_OK) (*out)->col_begin = col_begin;
     return rc;
@@ -314,8 +407,44 @@ int tcsc_gpu_plan_create_device(int rows, int cols, const int* d_csp, const int*
     HIP_TRY(hipMemcpyAsync(&ends[2], d_csn + col_begin, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(&ends[3], d_csn + col_end, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    return build_plan(rows, col_begin, col_end - col_begin, ends[1] - ends[0], ends[3] - ends[2], d_csp, d_csn,
-                      d_rip, d_rin, device, st, out);
+    // the same preconditions as tcsc_gpu_plan_create's host check, on the
+    // device: a bad range is an error, columns out of order are sorted
+    const int nc = col_end - col_begin;
+    DevBuf flag;
+    HIP_TRY(flag.alloc(sizeof(int)));
+    HIP_TRY(hipMemsetAsync(flag.p, 0, sizeof(int), st));
+    HIP_TRY(tcsc::check_index_device(d_csp, d_rip, col_begin, nc, rows, ends[1], flag.as<int>(), st));
+    HIP_TRY(tcsc::check_index_device(d_csn, d_rin, col_begin, nc, rows, ends[3], flag.as<int>(), st));
+    int hflag = 0;
+    HIP_TRY(hipMemcpyAsync(&hflag, flag.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (hflag & 1) {
+        set_error("tcsc_gpu_plan_create_device: a col_start range or a row index outside [0, %d)", rows);
+        return TCSC_E_ARG;
+    }
+    if (!(hflag & 2))
+        return build_plan(rows, col_begin, nc, ends[1] - ends[0], ends[3] - ends[2], d_csp, d_csn, d_rip, d_rin,
+                          device, st, out);
+    // columns out of order: rebased offsets and per-column sorted copies
+    const int np = ends[1] - ends[0], nn = ends[3] - ends[2];
+    DevBuf ocp, ocn, srp, srn, tmp;
+    HIP_TRY(ocp.alloc((size_t)(nc + 1) * sizeof(int)));
+    HIP_TRY(ocn.alloc((size_t)(nc + 1) * sizeof(int)));
+    HIP_TRY(srp.alloc((size_t)np * sizeof(int)));
+    HIP_TRY(srn.alloc((size_t)nn * sizeof(int)));
+    size_t tb1 = 0, tb2 = 0;
+    HIP_TRY(tcsc::sort_columns_tmp_bytes(np, nc, &tb1));
+    HIP_TRY(tcsc::sort_columns_tmp_bytes(nn, nc, &tb2));
+    const size_t tb = tb1 > tb2 ? tb1 : tb2;
+    HIP_TRY(tmp.alloc(tb));
+    HIP_TRY(tcsc::rebase_offsets(d_csp, col_begin, nc, ocp.as<int>(), st));
+    HIP_TRY(tcsc::rebase_offsets(d_csn, col_begin, nc, ocn.as<int>(), st));
+    HIP_TRY(tcsc::sort_columns(d_rip + ends[0], srp.as<int>(), np, nc, ocp.as<int>(), tmp.p, tb, st));
+    HIP_TRY(tcsc::sort_columns(d_rin + ends[2], srn.as<int>(), nn, nc, ocn.as<int>(), tmp.p, tb, st));
+    const int rc = build_plan(rows, 0, nc, np, nn, ocp.as<int>(), ocn.as<int>(), srp.as<int>(), srn.as<int>(), device,
+                              st, out);
+    if (rc == TCSC_OK) (*out)->col_begin = col_begin;
+    return rc;
 }
 
 int tcsc_gpu_plan_get_info(const tcsc_gpu_plan* p, tcsc_gpu_plan_info* info) {
@@ -359,6 +488,7 @@ int tcsc_gpu_plan_reserve(tcsc_gpu_plan* p, int max_M) {
     }
     p->ws = nullptr;
     p->ws_bytes = 0;
+    p->staged_M = -1;
     HIP_TRY(hipMalloc(&p->ws, want));
     p->ws_bytes = want;
     return TCSC_OK;
@@ -373,6 +503,7 @@ int tcsc_gpu_sgemm(const tcsc_gpu_plan* p, const float* dX, const float* dB, flo
         const int rc = tcsc_gpu_plan_reserve(const_cast<tcsc_gpu_plan*>(p), M);
         if (rc != TCSC_OK) return rc;
     }
+    if (p) const_cast<tcsc_gpu_plan*>(p)->staged_M = -1;  // this call's X^T replaces any staged one
     return sgemm_ws(p, dX, dB, dY, M, ldy, variant, a, stream, p ? p->ws : nullptr, p ? p->ws_bytes : 0);
 }
 
@@ -383,15 +514,24 @@ static int ensure_workspace(const tcsc_gpu_plan* p, int M) {
 }
 
 int tcsc_gpu_prepare_x(const tcsc_gpu_plan* p, const float* dX, int M, void* stream) {
-    const int rc = ensure_workspace(p, M);
+    int rc = ensure_workspace(p, M);
     if (rc != TCSC_OK) return rc;
-    return sgemm_ws(p, dX, nullptr, nullptr, M, 0, 0, 0.f, stream, p ? p->ws : nullptr, p ? p->ws_bytes : 0, 1);
+    if (p) const_cast<tcsc_gpu_plan*>(p)->staged_M = -1;
+    rc = sgemm_ws(p, dX, nullptr, nullptr, M, 0, 0, 0.f, stream, p ? p->ws : nullptr, p ? p->ws_bytes : 0, 1);
+    if (rc == TCSC_OK && p) const_cast<tcsc_gpu_plan*>(p)->staged_M = M;
+    return rc;
 }
 
 int tcsc_gpu_sgemm_prepared(const tcsc_gpu_plan* p, const float* dB, float* dY, int M, int ldy, int variant, float a,
                             void* stream) {
-    const int rc = ensure_workspace(p, M);
+    const int rc = ensure_workspace(p, M);  // a reallocation drops the staged X
     if (rc != TCSC_OK) return rc;
+    // the gather reads X^T with the pitch of the M it was staged for
+    if (p && M > 0 && p->cols > 0 && p->rows > 0 && p->staged_M != M) {
+        set_error("tcsc_gpu_sgemm_prepared: M=%d but %s (call tcsc_gpu_prepare_x with this M first)", M,
+                  p->staged_M < 0 ? "no X is staged" : "the staged X has another M");
+        return TCSC_E_ARG;
+    }
     return sgemm_ws(p, nullptr, dB, dY, M, ldy, variant, a, stream, p ? p->ws : nullptr, p ? p->ws_bytes : 0, 2);
 }
 
@@ -493,11 +633,13 @@ struct Shard {
 };
 
 struct CacheEntry {
-    // fingerprint: a tcsc_t is immutable after construction in the
-    // reference (SURVEY.md §8b "Ownership"); the fingerprint still guards
-    // against a caller rebuilding the arrays in place.
+    // fingerprint: the shape, the array addresses and a hash of the array
+    // contents (tcsc_fingerprint), checked on every call, so rebuilding the
+    // arrays in place or reusing freed addresses for another matrix gets a
+    // fresh plan
     int rows = 0, cols = 0, n_pos = 0, n_neg = 0;
     const int *csp = nullptr, *csn = nullptr, *rip = nullptr, *rin = nullptr;
+    uint64_t content = 0;
     std::vector<Shard> shards;
 };
 
@@ -518,10 +660,10 @@ void destroy_entry(CacheEntry& e) {
     e.shards.clear();
 }
 
-bool fingerprint_matches(const CacheEntry& e, const tcsc_t* W) {
+bool fingerprint_matches(const CacheEntry& e, const tcsc_t* W, uint64_t content) {
     return e.rows == W->rows && e.cols == W->cols && e.n_pos == W->n_elem_pos && e.n_neg == W->n_elem_neg &&
            e.csp == W->col_start_pos && e.csn == W->col_start_neg && e.rip == W->row_index_pos &&
-           e.rin == W->row_index_neg;
+           e.rin == W->row_index_neg && e.content == content;
 }
 
 [[noreturn]] void die() {
@@ -567,9 +709,10 @@ int get_entry_locked(const tcsc_t* W, CacheEntry** out) {
         return TCSC_E_NODEV;
     }
     if ((int)g_dev.size() < ndev) g_dev.resize(ndev);
+    const uint64_t content = tcsc_fingerprint(W);
     auto it = g_cache.find(W);
     if (it != g_cache.end()) {
-        if (fingerprint_matches(it->second, W)) {
+        if (fingerprint_matches(it->second, W, content)) {
             *out = &it->second;
             return TCSC_OK;
         }
@@ -585,6 +728,7 @@ int get_entry_locked(const tcsc_t* W, CacheEntry** out) {
     e.csn = W->col_start_neg;
     e.rip = W->row_index_pos;
     e.rin = W->row_index_neg;
+    e.content = content;
     int S = num_shards_locked(ndev);
     if (S > W->cols && W->cols > 0) S = W->cols;
     if (S < 1) S = 1;

@@ -33,7 +33,8 @@ constexpr int kCW = TCSC_CW;             // output columns per wave (4*kCW accum
 constexpr int kBatch = TCSC_BATCH;       // stream entries per batch (pipeline step, stream padding)
 constexpr int kWavesPerSimd = kWaves / 4;
 static_assert(kWaves % 4 == 0 && kWaves <= 16, "whole waves per SIMD");
-constexpr int kEntGuard = 64;            // entries allocated past the last stream (block loads)
+constexpr int kEntGuard = 64;            // entries allocated past the last stream (empty chain + block loads)
+constexpr int kHdr = 2;                  // header entries ahead of every (group, chunk) stream
 constexpr int kLdsBytes = kNBuf * kBufRows * kRowBytes;  // 147 KiB
 // Staging: waves 0..kDmaWaves-1 move a chunk, kDmaPerWave 1-KiB rows each,
 // right after the chunk loop's barrier (TCSC_DMA_EARLY=1) or after their
@@ -54,7 +55,13 @@ static_assert(kDmaWaves <= kWaves && kTK % kDmaWaves == 0, "each DMA wave moves 
 static_assert(kLdsBytes <= 160 * 1024, "LDS");
 static_assert(kNBuf == 2 || kNBuf == 3, "ring of 2 (DMA(c+1) before gather(c)) or 3 (DMA(c+2) after it)");
 
-// Stream entry (8 bytes): word0 = +1.0f or -1.0f (bit pattern), word1 =
+// Stream layout (v4).  Group-major: the streams of one wave-column group
+// follow each other chunk by chunk, each behind a header of kHdr entries
+// {nb, rem}, {byte distance to the next header, 0}, so a wave walks its
+// chain with one scalar add per chunk and reads its counts from the same
+// scalar loads that bring the entries (no stream table in the loop).
+// sptr[g*n_chunks + c] = entry index of the header of (g, c).
+// Entry (8 bytes): word0 = +1.0f or -1.0f (bit pattern), word1 =
 // (lds_row << 10) | (4*slot); lds_row = (chunk%3)*kBufRows + (k - chunk*kTK)
 // or the pad row; slot = column inside the wave (0..kCW-1).
 static_assert(4 * kCW <= 255, "slot index must fit the 8-bit gpr_idx field");
@@ -79,7 +86,7 @@ struct PlanOut {
     int n_groups = 0;          // ceil(ncols / kCW) wave-column groups
     long long n_entries = 0;   // stream entries incl. padding
     int2* ent = nullptr;       // n_entries (+kBatch) entries
-    int* sptr = nullptr;       // n_chunks*n_groups + 1 stream starts (entries)
+    int* sptr = nullptr;       // n_groups*n_chunks + 1 header positions (entries), group-major
     int* lbp = nullptr;
     int* lbn = nullptr;
     int* cnt = nullptr;
@@ -95,6 +102,7 @@ struct GemmArgs {
     int M = 0, K = 0;
     const int2* ent = nullptr;
     const int* sptr = nullptr;
+    long long n_entries = 0;   // the empty chain of idle waves starts here
     int n_groups = 0;
     int ncols = 0;
     long long nnz = 0;
@@ -126,6 +134,17 @@ hipError_t dense_to_tcsc_fill(const float* D, int rows, int cols, const int* csp
 // Y[m, n] = act(Y[m, n] + B[n]) in place (the dense baseline's epilogue)
 hipError_t launch_bias_act(float* Y, int M, int N, int ldy, const float* B, bool prelu, float a, hipStream_t st);
 hipError_t exclusive_scan_i32(const int* in, int* out, int n, void* tmp, size_t tmp_bytes, hipStream_t st);
+// Plan-build input checks on device TCSC arrays (tcsc_gpu_plan_create_device):
+// atomically ORs 1 into *d_flag for a bad col_start or a row outside
+// [0, rows), 2 for a column whose rows do not ascend.
+hipError_t check_index_device(const int* cs, const int* ri, int col_begin, int ncols, int rows, int n_total,
+                              int* d_flag, hipStream_t st);
+// out[j] = cs[col_begin + j] - cs[col_begin] for j in [0, ncols]
+hipError_t rebase_offsets(const int* cs, int col_begin, int ncols, int* out, hipStream_t st);
+// per-column ascending sort of row indices (segments off[j] .. off[j+1])
+hipError_t sort_columns_tmp_bytes(int n, int ncols, size_t* bytes);
+hipError_t sort_columns(const int* in, int* out, int n, int ncols, const int* off, void* tmp, size_t tmp_bytes,
+                        hipStream_t st);
 // X (M x K) -> XT (K x ldxt), rows m >= M zero; ldxt = ldxt_for(M) (M rounded up to kTM)
 int ldxt_for(int M);
 hipError_t launch_transpose(const float* X, int M, int K, float* XT, int ldxt, hipStream_t st);

@@ -49,7 +49,8 @@ typedef float f32x32 __attribute__((ext_vector_type(32)));
 #include "gather_asm.inc"
 #endif
 static_assert(TCSC_GEN_CW == kCW && TCSC_GEN_BATCH == kBatch, "generated loop geometry");
-static_assert(TCSC_GEN_CAP <= kEntGuard, "stream prefetch stays inside the entry guard");
+static_assert(TCSC_GEN_CAP + kHdr <= kEntGuard, "stream prefetch stays inside the entry guard");
+static_assert(TCSC_GEN_HDR == 2 * kHdr, "generated loop and plan agree on the chunk header");
 static_assert(TCSC_GEN_BUDGET == (512 / kWavesPerSimd) / 8 * 8, "generated loop VGPR budget");
 #ifndef TCSC_GEN_TAIL
 #define TCSC_GEN_TAIL 0
@@ -68,6 +69,15 @@ __device__ __forceinline__ int lower_bound_i32(const int* __restrict__ a, int lo
     while (lo < hi) {
         int mid = (lo + hi) >> 1;
         if (a[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// first position in a[lo, hi) with a[pos] > key
+__device__ __forceinline__ int upper_bound_i32(const int* __restrict__ a, int lo, int hi, int key) {
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (a[mid] <= key) lo = mid + 1; else hi = mid;
     }
     return lo;
 }
@@ -97,15 +107,16 @@ __global__ void k_chunk_counts(const int* __restrict__ lbp, const int* __restric
         cnt[i] = (lbp[i + ncols] - lbp[i]) + (lbn[i + ncols] - lbn[i]);
 }
 
-// gcnt[c*G + g] = entries of group g in chunk c, rounded up to kPad.
+// gcnt[g*nch + c] = entries of group g in chunk c (rounded up to kPad) plus
+// the chunk header: group-major, so one group's chunks follow each other.
 __global__ void k_group_counts(const int* __restrict__ cptr, int ncols, int nch, int G, int* __restrict__ gcnt) {
     const long long total = (long long)nch * G;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
          i += (long long)gridDim.x * blockDim.x) {
-        const int c = (int)(i / G), g = (int)(i % G);
+        const int g = (int)(i / nch), c = (int)(i % nch);
         const int n0 = g * kCW, n1 = min(n0 + kCW, ncols);
         const int real = cptr[(long long)c * ncols + n1] - cptr[(long long)c * ncols + n0];
-        gcnt[i] = (real + kPad - 1) / kPad * kPad;
+        gcnt[i] = kHdr + (real + kPad - 1) / kPad * kPad;
     }
 }
 
@@ -114,13 +125,17 @@ __device__ __forceinline__ int lds_row_of(int c, int k_local) { return (c % kNBu
 // Scatter the +1 (SIGN=0) or -1 (SIGN=1) entries to their stream slot.
 // Inside a (chunk, group) stream the columns follow each other and every
 // column's entries are in ascending row order (the +1/-1 lists merged), so
-// each output accumulates its nonzeros in ascending k.
+// each output accumulates its nonzeros in ascending k.  A row present in
+// both lists of a column (a hand-built tcsc_t; tcsc_from_dense never makes
+// one) puts its +1 entry first: a +1 entry counts the -1 entries with a
+// smaller row, a -1 entry the +1 entries with a smaller or equal row, so
+// every slot of the merged stream gets exactly one entry.
 template <int SIGN>
 __global__ void k_scatter(const int* __restrict__ cs_own, const int* __restrict__ ri_own,
                           const int* __restrict__ cs_oth, const int* __restrict__ ri_oth,
                           const int* __restrict__ lb_own, const int* __restrict__ lb_oth,
                           const int* __restrict__ cptr, const int* __restrict__ sptr, int col_begin, int ncols,
-                          int G, int2* __restrict__ ent) {
+                          int ent_nch, int2* __restrict__ ent) {
     const int base = cs_own[col_begin];
     const int total = cs_own[col_begin + ncols] - base;
     const int sgn = SIGN ? (int)0xbf800000u : 0x3f800000;
@@ -137,28 +152,70 @@ __global__ void k_scatter(const int* __restrict__ cs_own, const int* __restrict_
         const long long b = (long long)c * ncols + n;
         const int g = n / kCW, j = n - g * kCW;
         const int rank_own = i - lb_own[b];
-        const int rank_oth = lower_bound_i32(ri_oth, cs_oth[gn], cs_oth[gn + 1], k) - lb_oth[b];
+        const int rank_oth = (SIGN ? upper_bound_i32(ri_oth, cs_oth[gn], cs_oth[gn + 1], k)
+                                   : lower_bound_i32(ri_oth, cs_oth[gn], cs_oth[gn + 1], k)) - lb_oth[b];
         const int in_group = cptr[b] - cptr[(long long)c * ncols + g * kCW];
-        const int pos = sptr[(long long)c * G + g] + in_group + rank_own + rank_oth;
+        const int pos = sptr[(long long)g * (ent_nch) + c] + kHdr + in_group + rank_own + rank_oth;
         ent[pos] = make_int2(sgn, (lds_row_of(c, k - c * kTK) << 10) | (4 * j));
     }
 }
 
-// Padding entries: +1 x (the -0.0 row) -- an exact no-op on any accumulator.
-__global__ void k_fill_pads(const int* __restrict__ cptr, const int* __restrict__ sptr, int ncols, int nch, int G,
-                            int2* __restrict__ ent, long long n_entries) {
+// Chunk headers and padding.  Header of (group g, chunk c), kHdr entries
+// at sptr[g*nch + c]: {nb, rem} = the chunk's entries as whole batches +
+// the rest, {byte distance to the next chunk's header, 0}.  Padding
+// entries (padded streams only): +1 x (the -0.0 row), an exact no-op.
+// After the last stream: an empty chain for idle waves (a header of no
+// entries that points at itself), then guard entries that keep the
+// scalar-buffer loads past a stream's end inside the allocation.
+__global__ void k_fill_headers(const int* __restrict__ cptr, const int* __restrict__ sptr, int ncols, int nch, int G,
+                               int2* __restrict__ ent, long long n_entries) {
     const long long total = (long long)nch * G;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
          i += (long long)gridDim.x * blockDim.x) {
-        const int c = (int)(i / G), g = (int)(i % G);
+        const int g = (int)(i / nch), c = (int)(i % nch);
         const int n0 = g * kCW, n1 = min(n0 + kCW, ncols);
         const int real = cptr[(long long)c * ncols + n1] - cptr[(long long)c * ncols + n0];
         const int s0 = sptr[i], s1 = sptr[i + 1];
+        const int n = s1 - s0 - kHdr;
+        ent[s0] = make_int2(n / kBatch, n % kBatch);
+        ent[s0 + 1] = make_int2((s1 - s0) * (int)sizeof(int2), 0);
         const int2 pad = make_int2(0x3f800000, lds_row_of(c, kTK) << 10);
-        for (int p = s0 + real; p < s1; ++p) ent[p] = pad;
+        for (int p = s0 + kHdr + real; p < s1; ++p) ent[p] = pad;
     }
-    // trailing guard block (never consumed; keeps the 64-entry block loads in bounds)
-    if (blockIdx.x == 0 && threadIdx.x < kEntGuard) ent[n_entries + threadIdx.x] = make_int2(0x3f800000, kTK << 10);
+    if (blockIdx.x == 0 && threadIdx.x < kEntGuard)
+        ent[n_entries + threadIdx.x] = threadIdx.x < kHdr ? make_int2(0, 0) : make_int2(0x3f800000, kTK << 10);
+}
+
+// Plan-build precondition on device-resident TCSC arrays, one thread per
+// column of [col_begin, col_begin + ncols): col_start non-decreasing inside
+// [0, n_total], row indices in [0, rows) (flag bit 0 otherwise: the
+// reference would read outside X) and ascending (flag bit 1 otherwise: the
+// plan's merge by binary search needs them sorted).
+__global__ void k_check_index(const int* __restrict__ cs, const int* __restrict__ ri, int col_begin, int ncols,
+                              int rows, int n_total, int* __restrict__ flag) {
+    for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < ncols; n += gridDim.x * blockDim.x) {
+        const int a = cs[col_begin + n], b = cs[col_begin + n + 1];
+        int f = 0;
+        if (a < 0 || b < a || b > n_total) {
+            f = 1;
+        } else {
+            int prev = -1;
+            for (int i = a; i < b; ++i) {
+                const int k = ri[i];
+                if (k < 0 || k >= rows) f |= 1;
+                if (k < prev) f |= 2;
+                prev = k;
+            }
+        }
+        if (f) atomicOr(flag, f);
+    }
+}
+
+// out[j] = cs[col_begin + j] - cs[col_begin], j in [0, ncols]
+__global__ void k_rebase(const int* __restrict__ cs, int col_begin, int ncols, int* __restrict__ out) {
+    const int base = cs[col_begin];
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j <= ncols; j += gridDim.x * blockDim.x)
+        out[j] = cs[col_begin + j] - base;
 }
 
 // ---------------------------------------------------------------------------
@@ -228,32 +285,36 @@ __global__ void __launch_bounds__(256) k_transpose(const float* __restrict__ X, 
 
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(4))) const i32x16 const_i32x16;
+// the scalar buffer's last, 4- or 8-SGPR piece (header + CAP entries is not
+// a multiple of 16 dwords)
+typedef int sbuf_tail_t __attribute__((ext_vector_type(TCSC_SBUF_TAIL ? TCSC_SBUF_TAIL : 4)));
+typedef __attribute__((address_space(4))) const sbuf_tail_t const_sbuf_tail;
+static_assert(TCSC_GEN_TOUCH == 0, "the chunk loop passes no scalar-cache touch operands");
 
-// Consume this wave's stream for one chunk: `nb` whole batches of kBatch
-// entries, then `rem` more (the tail; TCSC_GEN_TAIL).
-// The first TCSC_GEN_CAP entries are already in the pinned SGPR buffer `sb`
-// (loaded by the caller's scalar loads); `ptr` is the stream's address, used
-// to reload the buffer for streams longer than the capacity.  The schedule
-// and register map are in tools/gen_gather_asm.py.
-// `tptr` is the next chunk's stream: its first scalar-cache lines are
-// touched at the start (loads into the pinned `junk` SGPR, never read), so
-// the real s_load after this gather hits in K$.  Whoever runs after the loop
-// must wait lgkmcnt(0) before the junk register is released.
-__device__ __forceinline__ void gather_stream(unsigned nb, unsigned rem, i32x16 (&sb)[TCSC_SBUF_VECS], unsigned long long ptr,
-                                              const void* tptr, int& junk, unsigned lane, unsigned mask,
+// Consume this wave's stream for one chunk.  The chunk's header {nb, rem,
+// bytes to the next header, 0} and first TCSC_GEN_CAP entries are already in
+// the pinned SGPR buffer (sb, sbt: the caller's scalar loads); `ptr` is the
+// header's address, from which the loop reloads the buffer for streams
+// longer than the capacity, and which it leaves at the NEXT chunk's header.
+// The schedule and register map are in tools/gen_gather_asm.py.
+__device__ __forceinline__ void gather_stream(i32x16 (&sb)[TCSC_SBUF_VECS], sbuf_tail_t& sbt,
+                                              unsigned long long& ptr, unsigned lane, unsigned mask,
                                               f32x32 (&acc)[TCSC_ACC_VECS]) {
+    (void)sbt;
     asm volatile(TCSC_GATHER_ASM
-                 : [nb] "+s"(nb), TCSC_ACC_OPERANDS(acc), TCSC_SBUF_OPERANDS(sb), TCSC_PTR_OPERAND(ptr),
-                   TCSC_JUNK_OPERAND(junk)
-                 : [lane] "v"(lane * 16u), [mask] "v"(mask), [tptr] "s"(tptr), [rem] "s"(rem)
+                 : TCSC_ACC_OPERANDS(acc), TCSC_SBUF_OPERANDS(sb, sbt), TCSC_PTR_OPERAND(ptr)
+                 : [lane] "v"(lane * 16u), [mask] "v"(mask)
                  : TCSC_GATHER_CLOBBERS);
 }
 
-// Scalar (SMEM) load of a stream's first TCSC_GEN_CAP entries.
-__device__ __forceinline__ void load_stream(i32x16 (&sb)[TCSC_SBUF_VECS], const int2* p) {
+// Scalar (SMEM) load of a chunk's header and its first TCSC_GEN_CAP entries.
+__device__ __forceinline__ void load_stream(i32x16 (&sb)[TCSC_SBUF_VECS], sbuf_tail_t& sbt, const char* p) {
     const_i32x16* q = reinterpret_cast<const_i32x16*>(reinterpret_cast<uintptr_t>(p));
 #pragma unroll
     for (int i = 0; i < TCSC_SBUF_VECS; ++i) sb[i] = q[i];
+#if TCSC_SBUF_TAIL
+    sbt = *reinterpret_cast<const_sbuf_tail*>(reinterpret_cast<uintptr_t>(p + 64 * TCSC_SBUF_VECS));
+#endif
 }
 
 // i is a compile-time constant after unrolling
@@ -365,8 +426,8 @@ __device__ __forceinline__ Tile xcd_tile() {
 template <bool BIAS_FIRST, bool PRELU, int OUT>
 __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd)
 k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __restrict__ ent,
-         const int* __restrict__ sptr, int G, int ncols, int nch, int chunks_per_slice, const float* __restrict__ Bias,
-         float* __restrict__ Y, int ldy, float a, float* __restrict__ ws) {
+         const int* __restrict__ sptr, long long n_entries, int G, int ncols, int nch, int chunks_per_slice,
+         const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a, float* __restrict__ ws) {
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -408,12 +469,13 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         // VMEM order is
         //   ... DMA(c) | DMA(c+1) | ...
         // so at the top of chunk c, vmcnt(kDmaPerWave) means DMA(c) has
-        // landed (entry streams are scalar loads, counted by lgkmcnt).  Ring of 2: DMA(c+1) is issued right after the barrier of
-        // chunk c (its buffer held chunk c-1), so it has gather(c) to land;
-        // the top of chunk c+1 waits vmcnt(0).  Either way the barrier makes
-        // every wave's rows of chunk c visible and says all waves are done
-        // with chunk c-1's buffer.  All loads in the loop are asm, so the
-        // compiler inserts no waits of its own.
+        // landed (entry streams are scalar loads, counted by lgkmcnt).  Ring
+        // of 2: DMA(c+1) is issued right after the barrier of chunk c (its
+        // buffer held chunk c-1), so it has gather(c) to land; the top of
+        // chunk c+1 waits vmcnt(0).  Either way the barrier makes every
+        // wave's rows of chunk c visible and says all waves are done with
+        // chunk c-1's buffer.  All loads in the loop are asm or scalar, so the
+        // compiler inserts no vmcnt waits of its own.
         DmaState dma;
         dma.chunk_bytes = (size_t)kTK * ldxt * 4;
         dma.next = reinterpret_cast<const char*>(XT + (size_t)c_begin * kTK * ldxt + m0);
@@ -423,149 +485,38 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                           (TCSC_DMA_OFFSET ? (unsigned)((i % 4) * kRowBytes) : 0u);
         dma.lds_wave = (unsigned)reinterpret_cast<uintptr_t>(lds) + (unsigned)(wave * kDmaPerWave * kRowBytes);
         const bool dma_wave = wave < kDmaWaves;  // uniform
-        int buf = c_begin % kNBuf;
-        if (dma_wave) dma_next_chunk(dma, buf);  // DMA(c_begin)
+        const int buf0 = c_begin % kNBuf;
+        if (dma_wave) dma_next_chunk(dma, buf0);  // DMA(c_begin)
 
-        const int gi = active ? g : G - 1;
-        int cb = c_begin;
-        long long ci = (long long)min(cb + lane, nch - 1) * G + gi;
-        int vs0 = sptr[ci], vs1 = sptr[ci + 1];
-        int s0n = __builtin_amdgcn_readfirstlane(vs0);
-        int s1n = __builtin_amdgcn_readfirstlane(vs1);
+        // This wave's chain of chunk streams (stream layout v4,
+        // tcsc_internal.h): the header of (g, c_begin); an idle wave (g >= G,
+        // last column block) walks the empty chain after the last stream.
+        unsigned long long cur = reinterpret_cast<unsigned long long>(
+            ent + (active ? (long long)sptr[(long long)g * nch + c_begin] : n_entries));
         i32x16 sb[TCSC_SBUF_VECS];
-        load_stream(sb, ent + s0n);
-        if (kNBuf == 3 && dma_wave) dma_next_chunk(dma, buf == 2 ? 0 : buf + 1);  // DMA(c_begin+1)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // pad rows
+        sbuf_tail_t sbt;
+        load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
+        if (kNBuf == 3 && dma_wave) dma_next_chunk(dma, buf0 == 2 ? 0 : buf0 + 1);  // DMA(c_begin+1)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                       // pad rows
 
         const unsigned mask = 0x3ffu;
-        int junk = 0;  // sink of the scalar-cache touches (gather_stream)
-#ifdef TCSC_STAMPS
-        // diagnostic build: shader-clock stamps around the waits (outputs are garbage)
-        unsigned long long st_bar = 0, st_dma = 0, st_smem = 0, st_gather = 0, st_t0 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef TCSC_TRACE
-        // diagnostic build: for kTraceN intervals from c_begin + kTrace0, per wave {top, barrier
-        // release, stream landed, gather end, batches, HW_ID}, parked in LDS (no VMEM in the
-        // loop) and copied into Y at the end (outputs are garbage)
-        constexpr int kTrace0 = 100, kTraceN = 32;
-        __shared__ unsigned trace_lds[kTraceN * kWaves * 6];
-        const unsigned hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-#endif
+        // ring buffer that DMA(c+2) (ring of 3) / DMA(c+1) (ring of 2) fills
+        int dbuf = kNBuf == 3 ? (buf0 == 0 ? 2 : buf0 - 1) : (buf0 ^ 1);
         for (int c = c_begin; c < c_end; ++c) {
-#ifdef TCSC_STAMPS
-            const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef TCSC_TRACE
-            const unsigned tr0 = (unsigned)__builtin_amdgcn_s_memtime();
-#endif
             // see the VMEM order above: ring of 3 keeps DMA(c+1) in flight
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kNBuf == 3 ? kDmaPerWave : 0) : "memory");
-#ifdef TCSC_STAMPS
-            const unsigned long long tbm = __builtin_amdgcn_s_memtime();
-            st_dma += tbm - tb0;
-#endif
             __builtin_amdgcn_s_barrier();
-#ifdef TCSC_STAMPS
-            const unsigned long long tb1 = __builtin_amdgcn_s_memtime();
-            st_bar += tb1 - tbm;
-#endif
-#ifdef TCSC_TRACE
-            const unsigned tr1 = (unsigned)__builtin_amdgcn_s_memtime();
-#endif
-            if (kNBuf == 2 && dma_wave) dma_next_chunk(dma, buf ^ 1);  // DMA(c+1) into the buffer chunk c-1 used
-            if (kNBuf == 3 && kDmaEarly && dma_wave) {
-                int b2 = buf + 2;
-                if (b2 >= 3) b2 -= 3;
-                dma_next_chunk(dma, b2);  // DMA(c+2) into the buffer chunk c-1 used (free since the barrier)
-            }
-            const int s0 = s0n, s1 = s1n;
-            const int idx = c + 1 - cb;
-            if (idx == 64) {  // next 64 chunks' stream bounds
-                cb += 64;
-                ci = (long long)min(cb + lane, nch - 1) * G + gi;
-                vs0 = sptr[ci];
-                vs1 = sptr[ci + 1];
-                s0n = __builtin_amdgcn_readfirstlane(vs0);
-                s1n = __builtin_amdgcn_readfirstlane(vs1);
-            } else {
-                s0n = __builtin_amdgcn_readlane(vs0, idx);
-                s1n = __builtin_amdgcn_readlane(vs1, idx);
-            }
-            const unsigned n_ent = active ? (unsigned)(s1 - s0) : 0u;
-            const unsigned nb = n_ent / kBatch, rem = n_ent % kBatch;  // whole batches, then the tail
-#ifdef TCSC_STAMPS
-            const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[36:51]}"(sb[0]), "+{s[52:67]}"(sb[1]), "+{s[68:83]}"(sb[2]));
-            const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
-            st_smem += ts1 - ts0;
-#endif
-#ifdef TCSC_TRACE
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[36:51]}"(sb[0]), "+{s[52:67]}"(sb[1]), "+{s[68:83]}"(sb[2]));
-            const unsigned trs = (unsigned)__builtin_amdgcn_s_memtime();
-#endif
-#if defined(TCSC_PRIO) && TCSC_PRIO
-            // longest stream first: the SIMD arbiter favours older waves, so a
-            // young wave with the most batches would otherwise finish last and
-            // hold the next barrier (tools/trace.py: gather time grows with slot)
-            if (nb >= (unsigned)(TCSC_PRIO + 2)) __builtin_amdgcn_s_setprio(3);
-            else if (nb >= (unsigned)(TCSC_PRIO + 1)) __builtin_amdgcn_s_setprio(2);
-            else if (nb >= (unsigned)TCSC_PRIO) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-#endif
-            gather_stream(nb, rem, sb, reinterpret_cast<unsigned long long>(ent + s0), ent + s0n, junk, lane, mask, acc);
-#ifdef TCSC_STAMPS
-            st_gather += __builtin_amdgcn_s_memtime() - ts1;
-#endif
-#ifdef TCSC_TRACE
-            {
-                const unsigned tr2 = (unsigned)__builtin_amdgcn_s_memtime();
-                const int ti = c - c_begin - kTrace0;
-                if (lane == 0 && ti >= 0 && ti < kTraceN) {
-                    unsigned* o = trace_lds + (ti * kWaves + wave) * 6;
-                    o[0] = tr0;
-                    o[1] = tr1;
-                    o[2] = trs;
-                    o[3] = tr2;
-                    o[4] = nb;
-                    o[5] = hwid;
-                }
-            }
-#endif
-            load_stream(sb, ent + s0n);  // next chunk's stream: lands behind the DMA issue and the barrier
-            if (kNBuf == 3 && !kDmaEarly && dma_wave) {
-                int b2 = buf + 2;
-                if (b2 >= 3) b2 -= 3;
-                dma_next_chunk(dma, b2);  // DMA(c+2) into the buffer chunk c-1 used
-            }
-            buf = buf == kNBuf - 1 ? 0 : buf + 1;
+            if ((kNBuf == 2 || kDmaEarly) && dma_wave) dma_next_chunk(dma, dbuf);
+            gather_stream(sb, sbt, cur, lane, mask, acc);  // leaves cur at the next chunk's header
+            // next chunk's stream: lands behind the DMA issue and the barrier
+            load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
+            // DMA(c+2) into the buffer chunk c-1 used
+            if (kNBuf == 3 && !kDmaEarly && dma_wave) dma_next_chunk(dma, dbuf);
+            dbuf = dbuf == kNBuf - 1 ? 0 : dbuf + 1;
         }
-#ifdef TCSC_STAMPS
-        const unsigned long long st_total = __builtin_amdgcn_s_memtime() - st_t0;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (lane == 0) {
-            const size_t wg = blockIdx.x + gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
-            unsigned* o = reinterpret_cast<unsigned*>(Y) + (wg * kWaves + wave) * 5;
-            o[0] = (unsigned)st_total;
-            o[1] = (unsigned)st_bar;
-            o[2] = (unsigned)st_smem;
-            o[3] = (unsigned)st_gather;
-            o[4] = (unsigned)st_dma;
-        }
-        return;
-#endif
-        // no LDS-DMA may still be writing when the workgroup's LDS is released,
-        // and no scalar-cache touch may land in the junk SGPR after its release
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+s"(junk)::"memory");
-#ifdef TCSC_TRACE
-        {
-            unsigned* o = reinterpret_cast<unsigned*>(Y) +
-                          ((blockIdx.x + gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z)) * kWaves + wave) *
-                              (size_t)kTraceN * 6;
-            for (int i = lane; i < kTraceN * 6; i += 64) o[i] = trace_lds[((i / 6) * kWaves + wave) * 6 + i % 6];
-        }
-        return;  // Y holds the trace
-#endif
+        // no LDS-DMA may still be writing when the workgroup's LDS is
+        // released, and the last (unused) stream load must have landed
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
 
     // Epilogue: lanes hold rows (4 per lane), so a direct store would put
@@ -785,16 +736,16 @@ hipError_t plan_fill(const PlanDev& in, PlanOut& out, hipStream_t st) {
     hipError_t e;
     if (in.n_pos > 0) {
         hipLaunchKernelGGL(k_scatter<0>, dim3(grid_for(in.n_pos, 256)), dim3(256), 0, st, in.csp, in.rip, in.csn,
-                           in.rin, out.lbp, out.lbn, out.cptr, out.sptr, in.col_begin, ncols, G, out.ent);
+                           in.rin, out.lbp, out.lbn, out.cptr, out.sptr, in.col_begin, ncols, nch, out.ent);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (in.n_neg > 0) {
         hipLaunchKernelGGL(k_scatter<1>, dim3(grid_for(in.n_neg, 256)), dim3(256), 0, st, in.csn, in.rin, in.csp,
-                           in.rip, out.lbn, out.lbp, out.cptr, out.sptr, in.col_begin, ncols, G, out.ent);
+                           in.rip, out.lbn, out.lbp, out.cptr, out.sptr, in.col_begin, ncols, nch, out.ent);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     const long long ng = (long long)nch * G;
-    hipLaunchKernelGGL(k_fill_pads, dim3(grid_for(ng, 256)), dim3(256), 0, st, out.cptr, out.sptr, ncols, nch, G,
+    hipLaunchKernelGGL(k_fill_headers, dim3(grid_for(ng, 256)), dim3(256), 0, st, out.cptr, out.sptr, ncols, nch, G,
                        out.ent, out.n_entries);
     return hipGetLastError();
 }
@@ -854,11 +805,11 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
     dim3 block(kWaves * 64);
     if (slices == 1) {
         hipLaunchKernelGGL((k_stream<BF, PR, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
-                           g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
+                           g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((k_stream<BF, PR, 1>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr, g.n_groups,
-                       g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
+    hipLaunchKernelGGL((k_stream<BF, PR, 1>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr, g.n_entries,
+                       g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const long long total = (long long)g.M * g.ncols;
@@ -909,6 +860,33 @@ hipError_t launch_bias_act(float* Y, int M, int N, int ldy, const float* B, bool
     else
         hipLaunchKernelGGL(k_bias_act<false>, dim3(grid_for(total, 256)), dim3(256), 0, st, Y, M, N, ldy, B, a);
     return hipGetLastError();
+}
+
+hipError_t check_index_device(const int* cs, const int* ri, int col_begin, int ncols, int rows, int n_total,
+                              int* d_flag, hipStream_t st) {
+    if (ncols <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_check_index, dim3(grid_for(ncols, 256)), dim3(256), 0, st, cs, ri, col_begin, ncols, rows,
+                       n_total, d_flag);
+    return hipGetLastError();
+}
+
+hipError_t rebase_offsets(const int* cs, int col_begin, int ncols, int* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_rebase, dim3(grid_for((long long)ncols + 1, 256)), dim3(256), 0, st, cs, col_begin, ncols, out);
+    return hipGetLastError();
+}
+
+hipError_t sort_columns_tmp_bytes(int n, int ncols, size_t* bytes) {
+    *bytes = 0;
+    return hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, *bytes, (const int*)nullptr, (int*)nullptr, n, ncols,
+                                                      (const int*)nullptr, (const int*)nullptr, 0, 32, (hipStream_t)0);
+}
+
+// Sort every column's row indices (segments off[j] .. off[j+1] of in, all
+// rows >= 0) into out.
+hipError_t sort_columns(const int* in, int* out, int n, int ncols, const int* off, void* tmp, size_t tmp_bytes,
+                        hipStream_t st) {
+    if (n <= 0 || ncols <= 0) return hipSuccess;
+    return hipcub::DeviceSegmentedRadixSort::SortKeys(tmp, tmp_bytes, in, out, n, ncols, off, off + 1, 0, 32, st);
 }
 
 hipError_t exclusive_scan_i32(const int* in, int* out, int n, void* tmp, size_t tmp_bytes, hipStream_t st) {

@@ -172,6 +172,44 @@ class TcscMatrix:
         buf = dense.reshape(-1) if dense.size else np.zeros(1, np.float32)
         return cls(lib().tcsc_from_dense(buf, rows, cols))
 
+    @classmethod
+    def from_arrays(cls, rows: int, cols: int, col_start_pos, col_start_neg, row_index_pos,
+                    row_index_neg) -> "TcscMatrix":
+        """A hand-built ``tcsc_t`` (the struct of sparse/tcsc.h:6-17) from four
+        index arrays, in malloc'd memory so that ``tcsc_free`` releases it as
+        it releases ``tcsc_from_dense``'s.  No checks here: the library's
+        plan build validates (rows in [0, rows), order) as the tests need."""
+        libc = C.CDLL(None)
+        libc.malloc.restype = C.c_void_p
+        libc.malloc.argtypes = [C.c_size_t]
+
+        def put(a):
+            a = np.ascontiguousarray(a, dtype=np.int32).reshape(-1)
+            p = libc.malloc(max(a.nbytes, 4))
+            if not p:
+                raise MemoryError("malloc failed")
+            if a.size:
+                C.memmove(p, a.ctypes.data, a.nbytes)
+            return C.cast(p, C.POINTER(C.c_int)), a.size
+
+        t = libc.malloc(C.sizeof(tcsc_t))
+        if not t:
+            raise MemoryError("malloc failed")
+        s = C.cast(t, C.POINTER(tcsc_t))
+        s.contents.rows, s.contents.cols = int(rows), int(cols)
+        s.contents.col_start_pos, _ = put(col_start_pos)
+        s.contents.col_start_neg, _ = put(col_start_neg)
+        s.contents.row_index_pos, s.contents.n_elem_pos = put(row_index_pos)
+        s.contents.row_index_neg, s.contents.n_elem_neg = put(row_index_neg)
+        return cls(s)
+
+    def row_index(self, sign: str) -> np.ndarray:
+        """Writable view of row_index_pos ('pos') or row_index_neg ('neg'):
+        lets tests rebuild the arrays in place, as a caller may."""
+        t = self.ptr.contents
+        p, n = (t.row_index_pos, t.n_elem_pos) if sign == "pos" else (t.row_index_neg, t.n_elem_neg)
+        return np.ctypeslib.as_array(p, shape=(n,)) if n > 0 else np.zeros(0, np.int32)
+
     @property
     def rows(self) -> int:
         return self.ptr.contents.rows
@@ -209,13 +247,31 @@ class TcscMatrix:
 
 def sgemm(variant: str, X: np.ndarray, W: TcscMatrix, B: np.ndarray, a: float = 0.2,
           Y: np.ndarray | None = None) -> np.ndarray:
-    """Host-pointer call of tcsc_sgemm_<variant> (sparse/tcsc.h:21-46)."""
+    """Host-pointer call of tcsc_sgemm_<variant> (sparse/tcsc.h:21-46).
+
+    The C entry points trust their sizes as the reference's do (they read N
+    floats of B and write M rows of pitch N into Y), so the shapes are checked
+    here and a mismatch raises :class:`TcscError` instead of reaching the
+    library as an out-of-bounds host read or write."""
+    if variant not in VARIANT_ID:
+        raise TcscError(f"unknown variant {variant!r} (one of {', '.join(VARIANTS)})")
+    if not getattr(W, "ptr", None):
+        raise TcscError("W is freed or not a TcscMatrix")
     X = np.ascontiguousarray(X, dtype=np.float32)
+    if X.ndim != 2:
+        raise TcscError(f"X must be 2-D (M x K), got shape {X.shape}")
     M, K = X.shape
     N = W.cols
+    if K != W.rows:
+        raise TcscError(f"X has K={K} columns but W has {W.rows} rows")
     B = np.ascontiguousarray(B, dtype=np.float32).reshape(-1)
+    if B.size != N:
+        raise TcscError(f"B has {B.size} elements, W has N={N} columns")
     if Y is None:
         Y = np.empty((M, N), np.float32)
+    elif (not isinstance(Y, np.ndarray) or Y.shape != (M, N) or Y.dtype != np.float32
+          or not Y.flags["C_CONTIGUOUS"]):
+        raise TcscError(f"Y must be a C-contiguous float32 array of shape ({M}, {N})")
     L = lib()
     nz = lambda a_: a_.reshape(-1) if a_.size else np.zeros(1, np.float32)  # noqa: E731
     if variant in PRELU_VARIANTS:

@@ -206,3 +206,45 @@ def test_mangled_aliases_forward_to_c_entry_points(built_lib, monkeypatch):
     assert cmp_x(y.ctypes.data_as(fp), z.ctypes.data_as(fp), 3, 5)
     z[1, 2] += 1e-3
     assert not cmp_x(y.ctypes.data_as(fp), z.ctypes.data_as(fp), 3, 5)
+
+
+def test_python_sgemm_checks_shapes_before_the_library(built_lib):
+    """The C entry points trust M, N, K as the reference's do; the Python
+    mirror raises on a mismatch instead of letting a short B or Y reach them."""
+    W = tcsc_amd.TcscMatrix.from_dense(np.eye(6, 5, dtype=np.float32))
+    X = np.ones((3, 6), np.float32)
+    with pytest.raises(tcsc_amd.TcscError, match="B has"):
+        tcsc_amd.sgemm("basic", X, W, np.zeros(4, np.float32))
+    with pytest.raises(tcsc_amd.TcscError, match="Y must be"):
+        tcsc_amd.sgemm("basic", X, W, np.zeros(5, np.float32), Y=np.zeros((3, 4), np.float32))
+    with pytest.raises(tcsc_amd.TcscError, match="Y must be"):
+        tcsc_amd.sgemm("basic", X, W, np.zeros(5, np.float32), Y=np.zeros((3, 5), np.float64))
+    with pytest.raises(tcsc_amd.TcscError, match="K=7"):
+        tcsc_amd.sgemm("basic", np.ones((3, 7), np.float32), W, np.zeros(5, np.float32))
+    with pytest.raises(tcsc_amd.TcscError, match="unknown variant"):
+        tcsc_amd.sgemm("fast", X, W, np.zeros(5, np.float32))
+    W.free()
+
+
+def test_hand_built_tcsc_round_trips_and_plan_build_validates_rows(built_lib, oracle):
+    """TcscMatrix.from_arrays (a malloc'd tcsc_t, freed by tcsc_free) keeps the
+    arrays; the plan build rejects a row outside [0, K) before touching a
+    device (the reference would read outside X)."""
+    Wd = oracle.ternary((40, 9), 0.2, 3)
+    ref = oracle.tcsc_from_dense(Wd)
+    W = tcsc_amd.TcscMatrix.from_arrays(40, 9, *ref.arrays())
+    for a, b in zip(W.arrays(), ref.arrays()):
+        np.testing.assert_array_equal(a, b)
+    W.free()
+    rip = ref.row_index_pos.copy()
+    rip[0] = 40
+    bad = tcsc_amd.TcscMatrix.from_arrays(40, 9, ref.col_start_pos, ref.col_start_neg, rip, ref.row_index_neg)
+    with pytest.raises(tcsc_amd.TcscError, match="outside"):
+        tcsc_amd.Plan(bad)
+    bad.free()
+    csn = ref.col_start_neg.copy()
+    csn[3], csn[4] = csn[4] + 1, csn[3]  # a decreasing col_start
+    bad = tcsc_amd.TcscMatrix.from_arrays(40, 9, ref.col_start_pos, csn, ref.row_index_pos, ref.row_index_neg)
+    with pytest.raises(tcsc_amd.TcscError, match="col_start_neg"):
+        tcsc_amd.Plan(bad)
+    bad.free()

@@ -9,7 +9,8 @@ gather for every stream length n (up to three SGPR buffers) and checks:
     uses the sign SGPRs and the gpr_idx word of the same entry as its data;
   * an X quad is not rewritten (v_bfi address or a new read) while a read
     into it is in flight or before both of its FMAs ran;
-  * reloads of the SGPR buffer (streams longer than CAP) advance by CAP.
+  * reloads of the SGPR buffer (streams longer than CAP) advance by CAP;
+  * every path ends by moving the pointer to the next chunk's header once.
 """
 import importlib.util
 import os
@@ -27,9 +28,10 @@ RE_DS = re.compile(r"ds_read_b128 v\[(\d+):(\d+)\], v(\d+)$")
 RE_WAIT = re.compile(r"s_waitcnt lgkmcnt\((\d+)\)$")
 RE_IDX = re.compile(r"s_set_gpr_idx_(?:on|idx) s(\d+)")
 RE_FMA = re.compile(r"v_pk_fma_f32 v\[(\d+):\d+\], v\[(\d+):\d+\], s\[(\d+):\d+\], v\[(\d+):\d+\] op_sel_hi:\[1,0,1\]$")
-RE_CMP = re.compile(r"s_cmp_eq_u32 %\[(nb|rem)\], (\d+)$")
-RE_SUB = re.compile(r"s_sub_u32 %\[nb\], %\[nb\], (\d+)$")
-RE_ADD = re.compile(r"s_add_u32 s(\d+), s(\d+), (\d+)$")
+RE_CMP = re.compile(r"s_cmp_eq_u32 (s\d+), (\d+)$")
+RE_SUB = re.compile(r"s_sub_u32 (s\d+), (s\d+), (\d+)$")
+RE_ADD = re.compile(r"s_add_u32 (s\d+), (s\d+), (\d+)$")
+RE_ADV = re.compile(r"s_add_u32 (s\d+), (s\d+), (s\d+)$")
 IGNORED = ("s_addc_u32", "s_load_dword", "s_set_gpr_idx_off")
 
 
@@ -37,9 +39,10 @@ def simulate(g, lines, nb, rem):
     """Run the loop for a stream of nb whole batches + rem entries; returns
     (reads, fmas): how often each entry index was read / FMA'd."""
     labels = {ln[:-1]: i for i, ln in enumerate(lines) if ln.endswith(":")}
-    ptr = g.slast + 1 + ((g.slast + 1) & 1)
+    ptr = f"s{g.ptr}"
     n = nb * g.batch + rem
-    regs = {"nb": nb, "rem": rem}
+    regs = {g.nb: nb, g.rem: rem}
+    advanced = 0
     base = 0  # stream index of SGPR slot 0
     scc = False
     addr, quad, pending = {}, {}, []  # address VGPR -> entry; quad -> [entry, landed, fmas]; reads in flight
@@ -98,12 +101,17 @@ def simulate(g, lines, nb, rem):
             quad[q][2] = done + 1
             fmas[e] = fmas.get(e, 0) + 1
         elif m := RE_SUB.match(ln):
-            regs["nb"] -= int(m[1])
+            assert m[1] == m[2] == g.nb
+            regs[g.nb] -= int(m[3])
         elif m := RE_ADD.match(ln):
-            assert int(m[1]) == int(m[2]) == ptr and int(m[3]) == 8 * g.cap
+            assert m[1] == m[2] == g.roff and int(m[3]) == 8 * g.cap, ln
             base += g.cap
+        elif m := RE_ADV.match(ln):
+            assert m[1] == m[2] == ptr and m[3] == g.next, ln
+            advanced += 1
         else:
             raise AssertionError(f"unexpected instruction {ln!r}")
+    assert advanced == 1, "the pointer must end at the next chunk's header, once"
     return reads, fmas
 
 

@@ -145,13 +145,15 @@ def test_prepare_then_gather_equals_sgemm(gpu, torch_cuda, name):
     Y1 = torch.empty((M, N), device=dev)
     plan.sgemm(X, B, Y1, M, N, "prelu_basic", 0.2, stream)
     plan.prepare_x(X, M, stream)
-    for variant in ("prelu_basic", "basic"):
-        Y2 = torch.empty((M, N), device=dev)
-        plan.sgemm_prepared(B, Y2, M, N, variant, 0.2, stream)
+    variants = ("prelu_basic", "basic")
+    Y2 = {v: torch.empty((M, N), device=dev) for v in variants}
+    for v in variants:  # one staging, several gathers
+        plan.sgemm_prepared(B, Y2[v], M, N, v, 0.2, stream)
+    for v in variants:
         Y3 = torch.empty((M, N), device=dev)
-        plan.sgemm(X, B, Y3, M, N, variant, 0.2, stream)
+        plan.sgemm(X, B, Y3, M, N, v, 0.2, stream)
         torch.cuda.synchronize()
-        np.testing.assert_array_equal(Y2.cpu().numpy(), Y3.cpu().numpy())
+        np.testing.assert_array_equal(Y2[v].cpu().numpy(), Y3.cpu().numpy())
     torch.cuda.synchronize()
     plan.destroy()
 
@@ -211,7 +213,10 @@ def test_shape_mismatch_reports_without_writing(gpu, monkeypatch):
     W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
     X = np.ones((4, 100), np.float32)  # K != W.rows
     Y = np.full((4, W.cols), 7.0, np.float32)
-    tcsc_amd.sgemm("basic", X, W, g["B"], 0.2, Y=Y)
+    with pytest.raises(tcsc_amd.TcscError, match="K=100"):  # the Python mirror checks first
+        tcsc_amd.sgemm("basic", X, W, g["B"], 0.2, Y=Y)
+    # the C entry point itself (as the reference's harness calls it)
+    gpu.tcsc_sgemm_basic(X.reshape(-1), W.ptr, np.ascontiguousarray(g["B"]), Y.reshape(-1), 4, W.cols, 100)
     assert np.all(Y == 7.0)
     assert "shape mismatch" in tcsc_amd.last_error()
 

@@ -9,13 +9,18 @@ is error-prone, and the geometry is a tuning knob: columns per wave CW
 (4*CW accumulator VGPRs), batch size, SGPR stream capacity CAP and the VGPR
 budget per wave (512 / waves per SIMD).
 
-Entries reach the wave as SCALARS.  A chunk's stream (8-byte entries
-{+-1.0f, (lds_row<<10) | 4*slot}) sits in SGPRs s36 .. s36+2*CAP-1 in memory
-order: the kernel's C++ loads the next chunk's first CAP entries with s_load
-right after the previous gather (the compiler's SMEM, waited before this
-asm; its latency hides behind the chunk barrier).  Streams longer than CAP
-reload the buffer in place between phases (s_load + lgkmcnt(0); rare at
-98 % sparsity).
+Entries reach the wave as SCALARS.  A chunk's stream (stream layout v4,
+csrc/tcsc_internal.h) is a 16-byte header {nb, rem, bytes to the next
+header, 0} and then 8-byte entries {+-1.0f, (lds_row<<10) | 4*slot}; the
+header and the first CAP entries sit in SGPRs s36 .. s39+2*CAP in memory
+order: the kernel's C++ loads them with s_load right after the previous
+gather (the compiler's SMEM, waited before this asm; its latency hides
+behind the chunk barrier).  The loop counts down the header's nb in place,
+reads rem from it, and ends by moving the pointer s[PTR:PTR+1] to the next
+chunk's header, so the C++ around it does no per-chunk arithmetic.
+Streams longer than CAP reload the entries in place between phases
+(s_load at the header's address + the header's scratch dword, which each
+reload advances by CAP entries; then lgkmcnt(0); rare at 98 % sparsity).
 
 Per batch p (BATCH entries, slots j = BATCH*p + i of the phase):
   ISSUE(p): v_bfi the per-lane LDS address (word's row bits + lane*16) into
@@ -29,7 +34,7 @@ under the FMAs of the DEPTH batches before it (DEPTH*BATCH reads stay in
 flight).  X quads cycle through DEPTH+1 register sets.
 
 Stream lengths (--tail):
-  1 (default) unpadded streams: %[nb] = whole batches, %[rem] = entries of
+  1 (default) unpadded streams: nb = whole batches, rem = entries of
     the last, partial batch.  Position p first checks whether the whole
     batches are used up and, if so, jumps to tail p, which issues only the
     rem reads of batch p, finishes batch p-1 and FMAs the rem entries
@@ -49,8 +54,9 @@ import sys
 
 
 class Geo:
-    def __init__(self, cw, batch, cap, budget, depth=1, touch=4, tail=1):
-        assert cw % 8 == 0 and cap % batch == 0 and 36 + 2 * cap <= 100
+    def __init__(self, cw, batch, cap, budget, depth=1, touch=4, tail=1, hdr=4):
+        assert cw % 8 == 0 and cap % batch == 0 and 36 + hdr + 2 * cap <= 100
+        assert hdr == 4 and (hdr + 2 * cap) % 4 == 0
         assert 1 <= depth and depth * batch <= 15, "lgkmcnt counts to 15"
         self.cw, self.batch, self.cap, self.budget, self.depth = cw, batch, cap, budget, depth
         self.touch = touch  # scalar-cache lines of the NEXT chunk's stream touched at the start
@@ -62,8 +68,15 @@ class Geo:
         self.acc = (self.xbase - nacc) & ~1
         assert self.acc >= 12, "VGPR budget too small for this geometry"
         self.xset = {k: self.xbase + 4 * batch * k for k in range(depth + 1)}
-        self.sbase = 36
-        self.slast = 36 + 2 * cap - 1
+        self.hdr = hdr  # chunk-header dwords ahead of the entries (stream layout v4)
+        self.sbuf = 36  # first SGPR of the scalar buffer: [header][CAP entries]
+        self.sbase = 36 + hdr
+        self.slast = 36 + hdr + 2 * cap - 1
+        # the chunk header in the buffer's first SGPRs: whole batches (the
+        # loop's countdown), the rest, bytes to the next header, and a
+        # scratch dword (0 in memory) the reloads use as their offset
+        self.nb, self.rem, self.next, self.roff = (f"s{36 + i}" for i in range(4))
+        self.ptr = self.slast + 1 + ((self.slast + 1) & 1)
 
 
 ABL = 0
@@ -108,28 +121,34 @@ def fma(g, p, wait, n=None):
     return out
 
 
-def count(p, target):
+def count(g, p, target):
     """After ISSUE(p): was batch p the phase's last one?  (nb is the number
     of batches left in this phase and beyond; 2 SALU, no decrement.)"""
-    return [f"s_cmp_eq_u32 %[nb], {p + 1}", f"s_cbranch_scc1 {target}"]
+    return [f"s_cmp_eq_u32 {g.nb}, {p + 1}", f"s_cbranch_scc1 {target}"]
 
 
 def reload(g):
-    """Next CAP entries of this stream into the buffer (phase > 0); the
-    stream pointer is pinned to s[PTR:PTR+1] (TCSC_PTR_OPERAND)."""
-    ptr = g.slast + 1 + ((g.slast + 1) & 1)
-    out = [f"s_add_u32 s{ptr}, s{ptr}, {8 * g.cap}", f"s_addc_u32 s{ptr + 1}, s{ptr + 1}, 0"]
+    """Next CAP entries of this stream into the buffer (phase > 0): from the
+    chunk header's address (s[PTR:PTR+1], TCSC_PTR_OPERAND, unchanged) plus
+    the header's scratch dword, advanced by CAP entries per phase."""
+    ptr = g.ptr
+    out = [f"s_add_u32 {g.roff}, {g.roff}, {8 * g.cap}"]
     nd = 2 * g.cap
-    off = 0
+    off = 4 * g.hdr  # the pointer is the chunk header's address
     r = g.sbase
     while nd > 0:
-        w = 16 if nd >= 16 else 8 if nd >= 8 else 4 if nd >= 4 else 2
-        out.append(f"s_load_dwordx{w} s[{r}:{r + w - 1}], s[{ptr}:{ptr + 1}], {hex(off)}")
+        w = 16 if nd >= 16 and r % 4 == 0 else 8 if nd >= 8 and r % 4 == 0 else 4 if nd >= 4 and r % 4 == 0 else 2
+        out.append(f"s_load_dwordx{w} s[{r}:{r + w - 1}], s[{ptr}:{ptr + 1}], {g.roff} offset:{hex(off)}")
         r += w
         off += 4 * w
         nd -= w
     out.append("s_waitcnt lgkmcnt(0)")
     return out
+
+
+def advance(g):
+    """Leave the pointer at the next chunk's header (the chain, stream layout v4)."""
+    return [f"s_add_u32 s{g.ptr}, s{g.ptr}, {g.next}", f"s_addc_u32 s{g.ptr + 1}, s{g.ptr + 1}, 0"]
 
 
 def generate(g):
@@ -153,16 +172,16 @@ def generate(g):
     for t in range(g.touch):
         off = min(64 * t, 8 * g.cap - 4)
         L.append(f"s_load_dword %[junk], %[tptr], {hex(off)}")
-    L += ["s_cmp_eq_u32 %[nb], 0", "s_cbranch_scc1 .Lend%="]
+    L += [f"s_cmp_eq_u32 {g.nb}, 0", "s_cbranch_scc1 .Lend%="]
     L.append(".Lphase%=:")
     for p in range(g.npos):
         L += issue(g, p)
         if p >= D:
             L += fma(g, p - D, g.batch * D)
-        L += count(p, f".Ldrain{p}%=")
+        L += count(g, p, f".Ldrain{p}%=")
     # a full phase done with batches left: finish its batches, reload, go on
     L += drain(g.npos - 1)
-    L.append(f"s_sub_u32 %[nb], %[nb], {g.npos}")
+    L.append(f"s_sub_u32 {g.nb}, {g.nb}, {g.npos}")
     L += reload(g)
     L.append("s_branch .Lphase%=")
     for p in range(g.npos):
@@ -171,7 +190,7 @@ def generate(g):
         if p != g.npos - 1:
             L.append("s_branch .Lend%=")
     L.append(".Lend%=:")
-    return L
+    return L + advance(g)
 
 
 def generate_tail(g):
@@ -187,20 +206,20 @@ def generate_tail(g):
     L = ["s_load_dword %[junk], %[tptr], " + hex(min(64 * t, 8 * g.cap - 4)) for t in range(g.touch)]
     L.append(".Lphase%=:")
     for p in range(g.npos):
-        L += [f"s_cmp_eq_u32 %[nb], {p}", f"s_cbranch_scc1 .Ltail{p}%="]
+        L += [f"s_cmp_eq_u32 {g.nb}, {p}", f"s_cbranch_scc1 .Ltail{p}%="]
         L += issue(g, p)
         if p >= D:
             L += fma(g, p - D, g.batch * D)
     # a full phase with batches left: finish its last batches, reload, go on
     for q in range(g.npos - D, g.npos):
         L += fma(g, q, g.batch * (g.npos - 1 - q))
-    L.append(f"s_sub_u32 %[nb], %[nb], {g.npos}")
+    L.append(f"s_sub_u32 {g.nb}, {g.nb}, {g.npos}")
     L += reload(g)
     L.append("s_branch .Lphase%=")
     for p in range(g.npos):
         L.append(f".Ltail{p}%=:")
         for r in range(g.batch - 1):
-            L += [f"s_cmp_eq_u32 %[rem], {r}", f"s_cbranch_scc1 .Lt{p}r{r}%="]
+            L += [f"s_cmp_eq_u32 {g.rem}, {r}", f"s_cbranch_scc1 .Lt{p}r{r}%="]
         for r in range(g.batch - 1, -1, -1):
             L.append(f".Lt{p}r{r}%=:")
             L += issue(g, p, r)
@@ -211,7 +230,7 @@ def generate_tail(g):
             if not (p == g.npos - 1 and r == 0):
                 L.append("s_branch .Lend%=")
     L.append(".Lend%=:")
-    return L
+    return L + advance(g)
 
 def emit(f, name, lines):
     f.write(f"#define {name} \\\n")
@@ -223,8 +242,10 @@ def emit(f, name, lines):
 def write_inc(path, g):
     global ABL
     nvec = 4 * g.cw // 32
-    nsv = 2 * g.cap // 16  # 16-SGPR vectors of the stream buffer
-    assert (2 * g.cap) % 16 == 0
+    ndw = g.hdr + 2 * g.cap      # scalar buffer: header + entries
+    nsv = ndw // 16              # 16-SGPR vectors of the buffer
+    stail = ndw % 16             # + one 4- or 8-SGPR vector
+    assert stail in (0, 4, 8)
     with open(path, "w") as f:
         f.write("// GENERATED by tools/gen_gather_asm.py -- do not edit by hand.\n")
         f.write(f"// geometry: cw={g.cw} batch={g.batch} cap={g.cap} vgpr budget={g.budget} depth={g.depth} "
@@ -232,13 +253,18 @@ def write_inc(path, g):
                 f"acc v[{g.acc}:{g.acc + 4 * g.cw - 1}], X v[{g.xbase}:{g.xbase + g.nx - 1}], "
                 f"stream s[{g.sbase}:{g.slast}]\n")
         f.write(f"#define TCSC_GEN_CW {g.cw}\n#define TCSC_GEN_BATCH {g.batch}\n#define TCSC_GEN_CAP {g.cap}\n")
+        f.write(f"#define TCSC_GEN_HDR {g.hdr}\n")
         f.write(f"#define TCSC_GEN_BUDGET {g.budget}\n#define TCSC_ACC_VECS {nvec}\n#define TCSC_SBUF_VECS {nsv}\n")
+        f.write(f"#define TCSC_SBUF_TAIL {stail}\n")
         f.write(f"#define TCSC_GEN_TAIL {int(g.tail)}\n")
         ops = ", ".join(f'"+{{v[{g.acc + 32 * i}:{g.acc + 32 * i + 31}]}}"(acc[{i}])' for i in range(nvec))
         f.write(f"#define TCSC_ACC_OPERANDS(acc) {ops}\n")
-        sops = ", ".join(f'"+{{s[{g.sbase + 16 * i}:{g.sbase + 16 * i + 15}]}}"(sb[{i}])' for i in range(nsv))
-        f.write(f"#define TCSC_SBUF_OPERANDS(sb) {sops}\n")
-        ptr = g.slast + 1 + ((g.slast + 1) & 1)
+        sops = ", ".join(f'"+{{s[{g.sbuf + 16 * i}:{g.sbuf + 16 * i + 15}]}}"(sb[{i}])' for i in range(nsv))
+        if stail:
+            t0 = g.sbuf + 16 * nsv
+            sops += f', "+{{s[{t0}:{t0 + stail - 1}]}}"(sbt)'
+        f.write(f"#define TCSC_SBUF_OPERANDS(sb, sbt) {sops}\n")
+        ptr = g.ptr
         f.write(f'#define TCSC_PTR_OPERAND(p) "+{{s[{ptr}:{ptr + 1}]}}"(p)\n')
         if g.touch:
             f.write(f'#define TCSC_JUNK_OPERAND(j) [junk] "+{{s{ptr + 2}}}"(j)\n')
@@ -267,11 +293,12 @@ def main():
     ap.add_argument("--depth", type=int, default=1)
     ap.add_argument("--touch", type=int, default=0)
     ap.add_argument("--tail", type=int, default=1)
+    ap.add_argument("--hdr", type=int, default=4, help="chunk-header dwords ahead of the entries")
     here = os.path.dirname(os.path.abspath(__file__))
     ap.add_argument("-o", default=os.path.join(here, "..", "sparse-matrix-multiplication-benchmark_amd", "csrc",
                                                "gather_asm.inc"))
     a = ap.parse_args()
-    write_inc(a.o, Geo(a.cw, a.batch, a.cap, a.budget, a.depth, a.touch, a.tail))
+    write_inc(a.o, Geo(a.cw, a.batch, a.cap, a.budget, a.depth, a.touch, a.tail, a.hdr))
     print(a.o)
 
 
