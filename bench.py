@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-dense-baseline", action="store_true", help="skip the rocBLAS dense comparison (N=1 only)")
     p.add_argument("--no-bcsr", action="store_true", help="skip the BCSR (1x8 blocks) line (N=1 only)")
+    p.add_argument("--no-reference-order", action="store_true",
+                   help="skip the reference-summation-order line (N=1 only)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
     p.add_argument("--override", default="", help="experiments only: e.g. 'K=16448,N=4096' (marks the line)")
     return p.parse_args()
@@ -238,6 +240,24 @@ def main():
             del Yd
         if Wd is not None and not args.no_bcsr:
             out["bcsr"] = bcsr_line(cfg, Wd, X, B, Y, nnz, gather_s, timed, sh, nsplit)
+        if world == 1 and not args.no_reference_order:
+            # include/tcsc_gpu.h TCSC_ORDER_REFERENCE: each variant in the reference's own
+            # summation order (float outputs bit-identical to sparse/tcsc.c); K is walked once
+            # per sign, so the gather is slower than the merged (fast) order the value uses
+            tcsc_amd.set_order("reference")
+            try:
+                rplan = tcsc_amd.Plan.from_device(cfg.K, ncols, csp, csn, rip, rin, 0, ncols, local_rank, sh)
+            finally:
+                tcsc_amd.set_order("fast")
+            rplan.reserve(cfg.M)
+            rplan.prepare_x(X, cfg.M, sh)
+            ref = {"kernel": "k_stream ORDER 1 / 2 (two sign chains)"}
+            for v in ("prelu_basic", "prelu_separate"):
+                rplan.sgemm_prepared(B, Y, cfg.M, ncols, v, 0.2, sh)
+                t = timed(lambda: rplan.sgemm_prepared(B, Y, cfg.M, ncols, v, 0.2, sh), nsplit)
+                ref[v] = {"ms": t * 1e3, "g_add_ops_per_s": adds_per_launch / t / 1e9, "vs_fast_order": t / gather_s}
+            rplan.destroy()
+            out["reference_order"] = ref
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, cfg, variant, X, B, csp, csn, rip[:npos], rin[:nneg])
         print(json.dumps(out), flush=True)

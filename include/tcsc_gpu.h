@@ -45,6 +45,20 @@ enum tcsc_status {
     TCSC_E_NODEV = 4     /* no usable gfx950 device                       */
 };
 
+/* Summation order of the gather.  FAST (default): each output column adds
+ * its +1 and -1 rows merged in ascending k; the five variants then agree with
+ * the reference within the fp32 bound of DESIGN.md "Numerics" and bit for bit
+ * on integer-valued inputs.  REFERENCE: the order of each reference variant
+ * (tcsc.c:84-93 for basic, :149-161 prelu_basic, :113-137 the optimized
+ * family), so float outputs are bit-identical to the reference compiled with
+ * IEEE semantics, at about twice the kernel time (K is walked once per
+ * sign).  Chosen per plan at creation time (tcsc_gpu_set_order, or
+ * TCSC_ORDER=reference in the environment). */
+enum tcsc_order {
+    TCSC_ORDER_FAST = 0,
+    TCSC_ORDER_REFERENCE = 1
+};
+
 typedef struct tcsc_gpu_plan tcsc_gpu_plan;
 
 typedef struct {
@@ -57,10 +71,17 @@ typedef struct {
     int chunk_k;         /* K rows per LDS chunk used by the kernel       */
     int n_chunks;        /* ceil(K / chunk_k)                             */
     size_t device_bytes; /* HBM held by the plan                          */
+    int order;           /* enum tcsc_order the plan was built for        */
 } tcsc_gpu_plan_info;
 
 /* Number of HIP devices visible (0 when there is no GPU). */
 int tcsc_gpu_device_count(void);
+
+/* Summation order for plans created from now on, including the plans the
+ * host-pointer API (sparse/tcsc.h) builds for its cache (a cached tcsc_t is
+ * rebuilt when the order changes).  Process-wide; default from $TCSC_ORDER. */
+void tcsc_gpu_set_order(int order);
+int tcsc_gpu_get_order(void);
 
 /* Upload columns [col_begin, col_end) of W to `device` and build the plan.
  * W is read on the host; `stream` orders the uploads and the build kernels.

@@ -45,6 +45,12 @@ struct tcsc_gpu_plan {
     // it), or -1 when nothing is staged: never staged, the workspace was
     // reallocated, or a whole tcsc_gpu_sgemm overwrote it with its own X
     int staged_M = -1;
+    // TCSC_ORDER_REFERENCE plans also carry the +1-only and -1-only chains
+    // (plans of the column range with one sign each), which the kernel walks
+    // one after the other in the reference's summation order
+    int order = TCSC_ORDER_FAST;
+    tcsc_gpu_plan* chain_pos = nullptr;
+    tcsc_gpu_plan* chain_neg = nullptr;
 };
 
 namespace {
@@ -171,6 +177,47 @@ int build_plan(int rows, int col_begin, int ncols, long long n_pos, long long n_
     plan->bytes = (size_t)(ng + 1) * sizeof(int) + (size_t)(total + tcsc::kEntGuard) * sizeof(int2);
     *out = plan.release();
     return TCSC_OK;
+}
+
+// Process-wide summation order for plans created from now on
+// (tcsc_gpu_set_order); initialised from $TCSC_ORDER ("reference" or "fast").
+std::mutex g_order_mu;
+int g_order = -1;
+
+int current_order() {
+    std::lock_guard<std::mutex> lk(g_order_mu);
+    if (g_order < 0) {
+        const char* e = std::getenv("TCSC_ORDER");
+        g_order = (e && std::strcmp(e, "reference") == 0) ? TCSC_ORDER_REFERENCE : TCSC_ORDER_FAST;
+    }
+    return g_order;
+}
+
+// The plan, plus -- in reference order -- its two one-sign chains: the same
+// build on the same arrays with the other sign's col_start replaced by zeros.
+int build_plan_ordered(int rows, int col_begin, int ncols, long long n_pos, long long n_neg, const int* csp,
+                       const int* csn, const int* rip, const int* rin, int device, hipStream_t st, int order,
+                       tcsc_gpu_plan** out) {
+    int rc = build_plan(rows, col_begin, ncols, n_pos, n_neg, csp, csn, rip, rin, device, st, out);
+    if (rc != TCSC_OK || order != TCSC_ORDER_REFERENCE) return rc;
+    tcsc_gpu_plan* p = *out;
+    p->order = order;
+    DevBuf zeros;
+    const size_t zb = (size_t)(col_begin + ncols + 1) * sizeof(int);
+    if (zeros.alloc(zb) != hipSuccess || hipMemsetAsync(zeros.p, 0, zb, st) != hipSuccess) {
+        tcsc_gpu_plan_destroy(p);
+        *out = nullptr;
+        set_error("tcsc_gpu_plan_create: cannot allocate the reference-order chains");
+        return TCSC_E_HIP;
+    }
+    rc = build_plan(rows, col_begin, ncols, n_pos, 0, csp, zeros.as<int>(), rip, rip, device, st, &p->chain_pos);
+    if (rc == TCSC_OK)
+        rc = build_plan(rows, col_begin, ncols, 0, n_neg, zeros.as<int>(), csn, rin, rin, device, st, &p->chain_neg);
+    if (rc != TCSC_OK) {
+        tcsc_gpu_plan_destroy(p);
+        *out = nullptr;
+    }
+    return rc;
 }
 
 // TCSC_SLICES=n forces the split-K factor (tests, tuning); read per call.
@@ -308,6 +355,17 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
     g.ent = p->ent;
     g.sptr = p->sptr;
     g.n_entries = p->n_entries;
+    if (p->order == TCSC_ORDER_REFERENCE && p->chain_pos && p->chain_neg) {
+        // basic / prelu_basic: one accumulator, +1 chain then -1 chain;
+        // the optimized family: the two sums apart (k_stream ORDER 2)
+        g.order = (variant == TCSC_VARIANT_BASIC || variant == TCSC_VARIANT_PRELU_BASIC) ? 1 : 2;
+        g.ent = p->chain_pos->ent;
+        g.sptr = p->chain_pos->sptr;
+        g.n_entries = p->chain_pos->n_entries;
+        g.ent2 = p->chain_neg->ent;
+        g.sptr2 = p->chain_neg->sptr;
+        g.n_entries2 = p->chain_neg->n_entries;
+    }
     g.n_groups = p->n_groups;
     g.ncols = p->cols;
     g.nnz = p->n_pos + p->n_neg;
@@ -381,8 +439,8 @@ int tcsc_gpu_plan_create(const tcsc_t* W, int col_begin, int col_end, int device
         HIP_TRY(hipMemcpyAsync(drip.p, hrip, (size_t)(p1 - p0) * sizeof(int), hipMemcpyHostToDevice, st));
     if (q1 > q0)
         HIP_TRY(hipMemcpyAsync(drin.p, hrin, (size_t)(q1 - q0) * sizeof(int), hipMemcpyHostToDevice, st));
-    rc = build_plan(W->rows, 0, nc, p1 - p0, q1 - q0, dcsp.as<int>(), dcsn.as<int>(), drip.as<int>(),
-                        drin.as<int>(), device, st, out);
+    rc = build_plan_ordered(W->rows, 0, nc, p1 - p0, q1 - q0, dcsp.as<int>(), dcsn.as<int>(), drip.as<int>(),
+                            drin.as<int>(), device, st, current_order(), out);
     if (rc == TCSC_OK) (*out)->col_begin = col_begin;
     return rc;
 }
@@ -423,8 +481,8 @@ int tcsc_gpu_plan_create_device(int rows, int cols, const int* d_csp, const int*
         return TCSC_E_ARG;
     }
     if (!(hflag & 2))
-        return build_plan(rows, col_begin, nc, ends[1] - ends[0], ends[3] - ends[2], d_csp, d_csn, d_rip, d_rin,
-                          device, st, out);
+        return build_plan_ordered(rows, col_begin, nc, ends[1] - ends[0], ends[3] - ends[2], d_csp, d_csn, d_rip,
+                                  d_rin, device, st, current_order(), out);
     // columns out of order: rebased offsets and per-column sorted copies
     const int np = ends[1] - ends[0], nn = ends[3] - ends[2];
     DevBuf ocp, ocn, srp, srn, tmp;
@@ -441,8 +499,8 @@ int tcsc_gpu_plan_create_device(int rows, int cols, const int* d_csp, const int*
     HIP_TRY(tcsc::rebase_offsets(d_csn, col_begin, nc, ocn.as<int>(), st));
     HIP_TRY(tcsc::sort_columns(d_rip + ends[0], srp.as<int>(), np, nc, ocp.as<int>(), tmp.p, tb, st));
     HIP_TRY(tcsc::sort_columns(d_rin + ends[2], srn.as<int>(), nn, nc, ocn.as<int>(), tmp.p, tb, st));
-    const int rc = build_plan(rows, 0, nc, np, nn, ocp.as<int>(), ocn.as<int>(), srp.as<int>(), srn.as<int>(), device,
-                              st, out);
+    const int rc = build_plan_ordered(rows, 0, nc, np, nn, ocp.as<int>(), ocn.as<int>(), srp.as<int>(),
+                                      srn.as<int>(), device, st, current_order(), out);
     if (rc == TCSC_OK) (*out)->col_begin = col_begin;
     return rc;
 }
@@ -461,9 +519,18 @@ int tcsc_gpu_plan_get_info(const tcsc_gpu_plan* p, tcsc_gpu_plan_info* info) {
     info->n_neg = p->n_neg;
     info->chunk_k = tcsc::kTK;
     info->n_chunks = p->n_chunks;
-    info->device_bytes = p->bytes + p->ws_bytes;
+    info->device_bytes = p->bytes + p->ws_bytes + (p->chain_pos ? p->chain_pos->bytes : 0) +
+                         (p->chain_neg ? p->chain_neg->bytes : 0);
+    info->order = p->order;
     return TCSC_OK;
 }
+
+void tcsc_gpu_set_order(int order) {
+    std::lock_guard<std::mutex> lk(g_order_mu);
+    g_order = order == TCSC_ORDER_REFERENCE ? TCSC_ORDER_REFERENCE : TCSC_ORDER_FAST;
+}
+
+int tcsc_gpu_get_order(void) { return current_order(); }
 
 void tcsc_gpu_plan_destroy(tcsc_gpu_plan* p) {
     if (!p) return;
@@ -471,6 +538,8 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan* p) {
     if (p->ent) (void)hipFree(p->ent);
     if (p->sptr) (void)hipFree(p->sptr);
     if (p->ws) (void)hipFree(p->ws);
+    tcsc_gpu_plan_destroy(p->chain_pos);
+    tcsc_gpu_plan_destroy(p->chain_neg);
     delete p;
 }
 
@@ -640,6 +709,7 @@ struct CacheEntry {
     int rows = 0, cols = 0, n_pos = 0, n_neg = 0;
     const int *csp = nullptr, *csn = nullptr, *rip = nullptr, *rin = nullptr;
     uint64_t content = 0;
+    int order = TCSC_ORDER_FAST;  // the summation order the shards' plans were built for
     std::vector<Shard> shards;
 };
 
@@ -663,7 +733,7 @@ void destroy_entry(CacheEntry& e) {
 bool fingerprint_matches(const CacheEntry& e, const tcsc_t* W, uint64_t content) {
     return e.rows == W->rows && e.cols == W->cols && e.n_pos == W->n_elem_pos && e.n_neg == W->n_elem_neg &&
            e.csp == W->col_start_pos && e.csn == W->col_start_neg && e.rip == W->row_index_pos &&
-           e.rin == W->row_index_neg && e.content == content;
+           e.rin == W->row_index_neg && e.content == content && e.order == current_order();
 }
 
 [[noreturn]] void die() {
@@ -729,6 +799,7 @@ int get_entry_locked(const tcsc_t* W, CacheEntry** out) {
     e.rip = W->row_index_pos;
     e.rin = W->row_index_neg;
     e.content = content;
+    e.order = current_order();
     int S = num_shards_locked(ndev);
     if (S > W->cols && W->cols > 0) S = W->cols;
     if (S < 1) S = 1;

@@ -103,6 +103,12 @@ struct GemmArgs {
     const int2* ent = nullptr;
     const int* sptr = nullptr;
     long long n_entries = 0;   // the empty chain of idle waves starts here
+    // summation order (k_stream ORDER): 0 merged (ent = the plan); 1, 2 the
+    // reference's orders (ent = the +1-only plan, ent2 = the -1-only plan)
+    int order = 0;
+    const int2* ent2 = nullptr;
+    const int* sptr2 = nullptr;
+    long long n_entries2 = 0;
     int n_groups = 0;
     int ncols = 0;
     long long nnz = 0;

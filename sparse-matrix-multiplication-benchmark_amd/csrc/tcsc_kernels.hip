@@ -423,11 +423,25 @@ __device__ __forceinline__ Tile xcd_tile() {
 }
 
 // OUT: 0 = final Y (bias + activation), 1 = partial slab ws[slice][M][ncols]
-template <bool BIAS_FIRST, bool PRELU, int OUT>
+// ORDER (the summation order, DESIGN.md "Numerics"):
+//   0  one plan, each column's +1 and -1 entries merged by ascending k;
+//   1  the reference's order for tcsc_sgemm_basic / _prelu_basic
+//      (tcsc.c:84-93, 149-161): the +1 chain (ent, all chunks) then the -1
+//      chain (ent2, all chunks) into the same accumulator;
+//   2  the reference's order for the optimized family (tcsc.c:113-137,
+//      184-216, 244-273): the +1 sums from 0 are added to the bias and
+//      parked in Y, the -1 chain sums from 0 again (its entries carry -1,
+//      so the sum is exactly -acc_neg), and the epilogue adds it to the
+//      parked value.
+// Orders 1 and 2 walk K twice (the X^T chunks are staged twice) and never
+// split K.
+template <bool BIAS_FIRST, bool PRELU, int OUT, int ORDER>
 __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd)
 k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __restrict__ ent,
-         const int* __restrict__ sptr, long long n_entries, int G, int ncols, int nch, int chunks_per_slice,
+         const int* __restrict__ sptr, long long n_entries, const int2* __restrict__ ent2,
+         const int* __restrict__ sptr2, long long n_entries2, int G, int ncols, int nch, int chunks_per_slice,
          const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a, float* __restrict__ ws) {
+    static_assert(ORDER == 0 || OUT == 0, "the reference orders do not split K");
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -457,12 +471,19 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     }
 
     // the -0.0 pad row of every ring buffer (entries padding a stream point here)
-    if (threadIdx.x < 64 * kNBuf) {
-        const int b = threadIdx.x >> 6;
-        reinterpret_cast<float4*>(lds + (b * kBufRows + kTK) * kRowBytes)[lane] = make_float4(-0.f, -0.f, -0.f, -0.f);
-    }
+    auto pad_rows = [&]() {
+        if (threadIdx.x < 64 * kNBuf) {
+            const int b = threadIdx.x >> 6;
+            reinterpret_cast<float4*>(lds + (b * kBufRows + kTK) * kRowBytes)[lane] =
+                make_float4(-0.f, -0.f, -0.f, -0.f);
+        }
+    };
+    pad_rows();
 
-    if (c_begin < c_end) {
+    // One walk over chunks [c_begin, c_end) of a plan's chains (stream
+    // layout v4) into acc.
+    auto run_chain = [&](const int2* __restrict__ e, const int* __restrict__ sp, long long ne) {
+        if (c_begin >= c_end) return;
         // Chunk c lives in ring buffer c % kNBuf (the plan baked that into
         // every entry).  Ring of 3: DMA(c+2) is issued right after gather(c),
         // so two chunks are in flight while one is consumed; per wave the
@@ -491,8 +512,8 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         // This wave's chain of chunk streams (stream layout v4,
         // tcsc_internal.h): the header of (g, c_begin); an idle wave (g >= G,
         // last column block) walks the empty chain after the last stream.
-        unsigned long long cur = reinterpret_cast<unsigned long long>(
-            ent + (active ? (long long)sptr[(long long)g * nch + c_begin] : n_entries));
+        unsigned long long cur =
+            reinterpret_cast<unsigned long long>(e + (active ? (long long)sp[(long long)g * nch + c_begin] : ne));
         i32x16 sb[TCSC_SBUF_VECS];
         sbuf_tail_t sbt;
         load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
@@ -517,7 +538,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         // no LDS-DMA may still be writing when the workgroup's LDS is
         // released, and the last (unused) stream load must have landed
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
+    };
 
     // Epilogue: lanes hold rows (4 per lane), so a direct store would put
     // 64 rows' 4-byte pieces in one instruction (partial-line writes that
@@ -526,86 +547,122 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     // (row stride kCW*4 + 16 B, so the b128 writes of consecutive lanes,
     // 4 rows apart, spread over the banks), then reads it back as rows:
     // kCW/4 lanes per row, 16-B stores.
-    __syncthreads();  // every wave is done with the tile ring
-    constexpr int kQ = kCW / 4;                 // 16-B quads per row
-    constexpr int kStride = kCW * 4 + 16;       // bytes per parked row
-    constexpr int kEpiRows = (kWaves * 128 * kStride <= kLdsBytes) ? 128 : 64;
-    static_assert(kWaves * kEpiRows * kStride <= kLdsBytes, "epilogue staging fits the LDS");
-    constexpr int kLanesPerPass = kEpiRows / 4;
-    constexpr int kRowsPerRead = 64 / kQ;       // rows one read instruction covers
-    char* region = lds + wave * (kEpiRows * kStride);
-    const int col0 = g * kCW;
-    const bool vec_ok = OUT == 0 ? ((ldy & 3) == 0 && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0))
-                                 : ((ncols & 3) == 0 && ((reinterpret_cast<uintptr_t>(ws) & 15) == 0));
+    // HOW: 0 the final values (bias last unless BIAS_FIRST, PReLU); 1 (order 2,
+    // after the +1 chain) acc + bias parked in Y as is; 2 (order 2, after the
+    // -1 chain) the parked value + acc, then PReLU.  A thread re-reads in
+    // HOW 2 exactly the elements it stored in HOW 1.
+    auto epilogue = [&](auto how_) {
+        constexpr int HOW = decltype(how_)::value;
+        __syncthreads();  // every wave is done with the tile ring
+        constexpr int kQ = kCW / 4;                 // 16-B quads per row
+        constexpr int kStride = kCW * 4 + 16;       // bytes per parked row
+        constexpr int kEpiRows = (kWaves * 128 * kStride <= kLdsBytes) ? 128 : 64;
+        static_assert(kWaves * kEpiRows * kStride <= kLdsBytes, "epilogue staging fits the LDS");
+        constexpr int kLanesPerPass = kEpiRows / 4;
+        constexpr int kRowsPerRead = 64 / kQ;       // rows one read instruction covers
+        char* region = lds + wave * (kEpiRows * kStride);
+        const int col0 = g * kCW;
+        const bool vec_ok = OUT == 0 ? ((ldy & 3) == 0 && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0))
+                                     : ((ncols & 3) == 0 && ((reinterpret_cast<uintptr_t>(ws) & 15) == 0));
+        constexpr bool kAddBias = OUT == 0 && (HOW == 1 || (HOW == 0 && !BIAS_FIRST));
+        constexpr bool kPrelu = PRELU && HOW != 1;
 #pragma unroll
-    for (int h = 0; h < 256 / kEpiRows; ++h) {
-        if (active && lane / kLanesPerPass == h) {
-            const int lh = lane % kLanesPerPass;
+        for (int h = 0; h < 256 / kEpiRows; ++h) {
+            if (active && lane / kLanesPerPass == h) {
+                const int lh = lane % kLanesPerPass;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int R = 4 * lh + r;
+                for (int r = 0; r < 4; ++r) {
+                    const int R = 4 * lh + r;
 #pragma unroll
-                for (int q = 0; q < kQ; ++q) {
-                    const float4 v = make_float4(acc_get(acc, 4 * (4 * q + 0) + r), acc_get(acc, 4 * (4 * q + 1) + r),
-                                                 acc_get(acc, 4 * (4 * q + 2) + r), acc_get(acc, 4 * (4 * q + 3) + r));
-                    *reinterpret_cast<float4*>(region + R * kStride + q * 16) = v;
+                    for (int q = 0; q < kQ; ++q) {
+                        const float4 v =
+                            make_float4(acc_get(acc, 4 * (4 * q + 0) + r), acc_get(acc, 4 * (4 * q + 1) + r),
+                                        acc_get(acc, 4 * (4 * q + 2) + r), acc_get(acc, 4 * (4 * q + 3) + r));
+                        *reinterpret_cast<float4*>(region + R * kStride + q * 16) = v;
+                    }
                 }
             }
-        }
-        __syncthreads();
-        if (active && lane < kRowsPerRead * kQ) {
-            const int q = lane % kQ;
-            const int col = col0 + 4 * q;
-            float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (OUT == 0 && !BIAS_FIRST) {
-                bq.x = col + 0 < ncols ? Bias[col + 0] : 0.f;
-                bq.y = col + 1 < ncols ? Bias[col + 1] : 0.f;
-                bq.z = col + 2 < ncols ? Bias[col + 2] : 0.f;
-                bq.w = col + 3 < ncols ? Bias[col + 3] : 0.f;
-            }
+            __syncthreads();
+            if (active && lane < kRowsPerRead * kQ) {
+                const int q = lane % kQ;
+                const int col = col0 + 4 * q;
+                float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (kAddBias) {
+                    bq.x = col + 0 < ncols ? Bias[col + 0] : 0.f;
+                    bq.y = col + 1 < ncols ? Bias[col + 1] : 0.f;
+                    bq.z = col + 2 < ncols ? Bias[col + 2] : 0.f;
+                    bq.w = col + 3 < ncols ? Bias[col + 3] : 0.f;
+                }
 #pragma unroll 4
-            for (int i = 0; i < (kEpiRows + kRowsPerRead - 1) / kRowsPerRead; ++i) {
-                const int R = lane / kQ + kRowsPerRead * i;
-                const int row = m0 + kEpiRows * h + R;
-                if (R >= kEpiRows) break;
-                float4 v = *reinterpret_cast<const float4*>(region + R * kStride + q * 16);
-                if (row < M && col < ncols) {
-                    float* dst;
-                    if (OUT == 0) {
-                        if (!BIAS_FIRST) {
-                            v.x += bq.x;
-                            v.y += bq.y;
-                            v.z += bq.z;
-                            v.w += bq.w;
-                        }
-                        if (PRELU) {
-                            v.x = (v.x < 0.0f) ? a * v.x : v.x;
-                            v.y = (v.y < 0.0f) ? a * v.y : v.y;
-                            v.z = (v.z < 0.0f) ? a * v.z : v.z;
-                            v.w = (v.w < 0.0f) ? a * v.w : v.w;
-                        }
-                        dst = Y + (size_t)row * ldy + col;
-                    } else {
-                        dst = ws + ((size_t)t.z * M + row) * ncols + col;
-                    }
-                    if (vec_ok && col + 3 < ncols) {
-                        if (OUT == 0) {  // Y is never re-read here: keep it out of L2's way
-                            typedef float nt4 __attribute__((ext_vector_type(4)));
-                            nt4 w = {v.x, v.y, v.z, v.w};
-                            __builtin_nontemporal_store(w, reinterpret_cast<nt4*>(dst));
+                for (int i = 0; i < (kEpiRows + kRowsPerRead - 1) / kRowsPerRead; ++i) {
+                    const int R = lane / kQ + kRowsPerRead * i;
+                    const int row = m0 + kEpiRows * h + R;
+                    if (R >= kEpiRows) break;
+                    float4 v = *reinterpret_cast<const float4*>(region + R * kStride + q * 16);
+                    if (row < M && col < ncols) {
+                        float* dst;
+                        if (OUT == 0) {
+                            dst = Y + (size_t)row * ldy + col;
+                            if (HOW == 2) {  // the parked bias + (+1 sums), then + (-1 sums)
+                                const bool full = vec_ok && col + 3 < ncols;
+                                v.x = dst[0] + v.x;
+                                v.y = (full || col + 1 < ncols) ? dst[1] + v.y : v.y;
+                                v.z = (full || col + 2 < ncols) ? dst[2] + v.z : v.z;
+                                v.w = (full || col + 3 < ncols) ? dst[3] + v.w : v.w;
+                            }
+                            if (kAddBias) {
+                                v.x += bq.x;
+                                v.y += bq.y;
+                                v.z += bq.z;
+                                v.w += bq.w;
+                            }
+                            if (kPrelu) {
+                                v.x = (v.x < 0.0f) ? a * v.x : v.x;
+                                v.y = (v.y < 0.0f) ? a * v.y : v.y;
+                                v.z = (v.z < 0.0f) ? a * v.z : v.z;
+                                v.w = (v.w < 0.0f) ? a * v.w : v.w;
+                            }
                         } else {
-                            *reinterpret_cast<float4*>(dst) = v;
+                            dst = ws + ((size_t)t.z * M + row) * ncols + col;
                         }
-                    } else {
-                        dst[0] = v.x;
-                        if (col + 1 < ncols) dst[1] = v.y;
-                        if (col + 2 < ncols) dst[2] = v.z;
-                        if (col + 3 < ncols) dst[3] = v.w;
+                        if (vec_ok && col + 3 < ncols) {
+                            if (OUT == 0 && HOW != 1) {  // Y is never re-read here: keep it out of L2's way
+                                typedef float nt4 __attribute__((ext_vector_type(4)));
+                                nt4 w = {v.x, v.y, v.z, v.w};
+                                __builtin_nontemporal_store(w, reinterpret_cast<nt4*>(dst));
+                            } else {
+                                *reinterpret_cast<float4*>(dst) = v;
+                            }
+                        } else {
+                            dst[0] = v.x;
+                            if (col + 1 < ncols) dst[1] = v.y;
+                            if (col + 2 < ncols) dst[2] = v.z;
+                            if (col + 3 < ncols) dst[3] = v.w;
+                        }
                     }
                 }
             }
+            if (h + 1 < 256 / kEpiRows) __syncthreads();  // region reused by the next pass
         }
-        if (h + 1 < 256 / kEpiRows) __syncthreads();  // region reused by the next pass
+    };
+
+    run_chain(ent, sptr, n_entries);
+    if constexpr (ORDER == 0) {
+        epilogue(std::integral_constant<int, 0>{});
+    } else if constexpr (ORDER == 1) {
+        __syncthreads();  // every wave is done with the ring before the -1 chain refills it
+        run_chain(ent2, sptr2, n_entries2);
+        epilogue(std::integral_constant<int, 0>{});
+    } else {
+        epilogue(std::integral_constant<int, 1>{});
+#pragma unroll
+        for (int v = 0; v < TCSC_ACC_VECS; ++v)
+#pragma unroll
+            for (int i = 0; i < 32; ++i) acc[v][i] = 0.f;
+        __syncthreads();  // the epilogue's LDS staging is done before the ring is refilled
+        pad_rows();
+        run_chain(ent2, sptr2, n_entries2);
+        epilogue(std::integral_constant<int, 2>{});
     }
 }
 
@@ -798,18 +855,32 @@ int choose_slices(int M, int ncols, int K, long long nnz, int G, size_t ws_bytes
 template <bool BF, bool PR>
 static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
     const int nch = (g.K + kTK - 1) / kTK;
+    if (g.order != 0) slices = 1;  // the reference orders walk K in order
     int cps = nch > 0 ? (nch + slices - 1) / slices : 1;
     slices = nch > 0 ? (nch + cps - 1) / cps : 1;
     const int ldxt = ldxt_of(g.M);
     dim3 grid((g.n_groups + kWaves - 1) / kWaves, (g.M + kTM - 1) / kTM, slices);
     dim3 block(kWaves * 64);
-    if (slices == 1) {
-        hipLaunchKernelGGL((k_stream<BF, PR, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
-                           g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
+    if (g.order == 1) {
+        hipLaunchKernelGGL((k_stream<BF, PR, 0, 1>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
+                           g.n_entries, g.ent2, g.sptr2, g.n_entries2, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy,
+                           g.a, g.ws);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((k_stream<BF, PR, 1>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr, g.n_entries,
-                       g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
+    if (g.order == 2) {
+        hipLaunchKernelGGL((k_stream<false, PR, 0, 2>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
+                           g.n_entries, g.ent2, g.sptr2, g.n_entries2, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy,
+                           g.a, g.ws);
+        return hipGetLastError();
+    }
+    if (slices == 1) {
+        hipLaunchKernelGGL((k_stream<BF, PR, 0, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
+                           g.n_entries, g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy,
+                           g.a, g.ws);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL((k_stream<BF, PR, 1, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr, g.n_entries,
+                       g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const long long total = (long long)g.M * g.ncols;

@@ -40,7 +40,8 @@ EXPORTED_SYMBOLS = (
     "tcsc_gpu_device_count", "tcsc_gpu_plan_create", "tcsc_gpu_plan_create_device", "tcsc_gpu_plan_get_info",
     "tcsc_gpu_plan_reserve", "tcsc_gpu_plan_destroy", "tcsc_gpu_sgemm", "tcsc_gpu_prepare_x",
     "tcsc_gpu_sgemm_prepared", "tcsc_gpu_from_dense", "tcsc_gpu_dense_sgemm", "tcsc_gpu_last_error",
-    "tcsc_gpu_cache_clear", "tcsc_gpu_num_shards", "tcsc_gpu_set_num_shards",
+    "tcsc_gpu_cache_clear", "tcsc_gpu_num_shards", "tcsc_gpu_set_num_shards", "tcsc_gpu_set_order",
+    "tcsc_gpu_get_order",
     # include/sparse/bcsr.h
     "bcsr_from_dense", "bcsr_sgemm_basic", "bcsr_sgemm_prelu_basic", "bcsr_sgemm_avx", "bcsr_sgemm_prelu_avx",
     "bcsr_sgemm_avx2", "bcsr_free",
@@ -68,7 +69,7 @@ class plan_info_t(C.Structure):
     _fields_ = [
         ("device", C.c_int), ("rows", C.c_int), ("cols", C.c_int), ("col_begin", C.c_int),
         ("nnz", C.c_longlong), ("n_pos", C.c_longlong), ("n_neg", C.c_longlong),
-        ("chunk_k", C.c_int), ("n_chunks", C.c_int), ("device_bytes", C.c_size_t),
+        ("chunk_k", C.c_int), ("n_chunks", C.c_int), ("device_bytes", C.c_size_t), ("order", C.c_int),
     ]
 
 
@@ -132,6 +133,9 @@ def lib():
     L.tcsc_gpu_set_num_shards.argtypes = [i]
     L.tcsc_gpu_set_num_shards.restype = None
     L.tcsc_gpu_cache_clear.restype = None
+    L.tcsc_gpu_set_order.argtypes = [i]
+    L.tcsc_gpu_set_order.restype = None
+    L.tcsc_gpu_get_order.restype = i
     from . import bcsr as _bcsr
 
     _bcsr.bind(L)
@@ -281,6 +285,20 @@ def sgemm(variant: str, X: np.ndarray, W: TcscMatrix, B: np.ndarray, a: float = 
     else:
         getattr(L, "tcsc_sgemm_" + variant)(nz(X), W.ptr, nz(B), nz(Y), M, N, K)
     return Y
+
+
+ORDERS = {"fast": 0, "reference": 1}
+
+
+def set_order(order: str) -> None:
+    """Summation order of plans created from now on (include/tcsc_gpu.h
+    tcsc_order): "fast" (merged +1/-1, tolerance parity) or "reference"
+    (each variant's own order: float outputs bit-identical to the reference)."""
+    lib().tcsc_gpu_set_order(ORDERS[order])
+
+
+def get_order() -> str:
+    return {v: k for k, v in ORDERS.items()}[int(lib().tcsc_gpu_get_order())]
 
 
 def set_num_shards(n: int) -> None:
