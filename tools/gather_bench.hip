@@ -10,6 +10,10 @@
 //   mode 3        a 16-dword scalar prefetch issued BEFORE every call and
 //                 waited after it: what an SMEM load in flight costs the
 //                 gather's lgkmcnt-counted LDS pipeline
+//   mode 4..6     skewed work: wave w gets n * f[w / 4] entries (same mean),
+//                 f = {1.3, 1.1, 0.9, 0.7} / {0.7, 0.9, 1.1, 1.3} /
+//                 {1.15, 1.05, 0.95, 0.85}: do older waves (the SIMD arbiter
+//                 favours them) finish with the younger ones if they get more?
 //   Build: hipcc --offload-arch=gfx950 -O3 -I../sparse-matrix-multiplication-benchmark_amd/csrc -o gather_bench gather_bench.hip
 //   Run:   ./gather_bench [N entries per stream (<= 30 for modes 1-3)] [barrier 0/1] [mode]
 #include <hip/hip_runtime.h>
@@ -95,7 +99,7 @@ int main(int argc, char** argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 16;
     const int bar = argc > 2 ? atoi(argv[2]) : 0;
     const int mode = argc > 3 ? atoi(argv[3]) : 0;
-    if (mode && n > 30) {
+    if (mode >= 1 && mode <= 3 && n > 30) {
         printf("modes 1-3 keep streams of at most 30 entries\n");
         return 1;
     }
@@ -104,20 +108,23 @@ int main(int argc, char** argv) {
     const int cus = prop.multiProcessorCount;
     // per wave: header {nb, rem, next = 0, 0} + entries (+ slack for the
     // scalar buffer), or kSlots copies 64 ints apart for the reload modes
-    const int ints = mode ? kSlots * 64 : 4 + 2 * (n + 64);
-    const int ne = mode ? 30 : n + 64;
+    const bool slots = mode >= 1 && mode <= 3;
+    const int ints = slots ? kSlots * 64 : 4 + 2 * (2 * n + 64);
+    const int ne = slots ? 30 : 2 * n + 64;
     std::vector<int> h((size_t)cus * kWaves * ints, 0);
     srand(1);
     for (int w = 0; w < cus * kWaves; ++w) {
         int* s = h.data() + (size_t)w * ints;
-        s[0] = n / TCSC_GEN_BATCH;
-        s[1] = n % TCSC_GEN_BATCH;
+        static const float skew[3][4] = {{1.3f, 1.1f, 0.9f, 0.7f}, {0.7f, 0.9f, 1.1f, 1.3f}, {1.15f, 1.05f, 0.95f, 0.85f}};
+        const int nw = mode >= 4 ? (int)(n * skew[mode - 4][(w % kWaves) / 4] + 0.5f) : n;
+        s[0] = nw / TCSC_GEN_BATCH;
+        s[1] = nw % TCSC_GEN_BATCH;
         for (int j = 0; j < ne; ++j) {
             const int row = rand() % kRows, slot = rand() % TCSC_GEN_CW;
             s[4 + 2 * j] = (rand() & 1) ? 0x3f800000 : (int)0xbf800000;
             s[4 + 2 * j + 1] = (row << 10) | (4 * slot);
         }
-        if (mode)
+        if (slots)
             for (int k = 1; k < kSlots; ++k)
                 for (int i = 0; i < 64; ++i) s[k * 64 + i] = s[i];
     }
