@@ -56,6 +56,7 @@ def parse():
     p.add_argument("--no-bcsr", action="store_true", help="skip the BCSR (1x8 blocks) line (N=1 only)")
     p.add_argument("--no-reference-order", action="store_true",
                    help="skip the reference-summation-order line (N=1 only)")
+    p.add_argument("--no-validate", action="store_true", help="skip the pre-timing check against the dense product")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
     p.add_argument("--override", default="", help="experiments only: e.g. 'K=16448,N=4096' (marks the line)")
     return p.parse_args()
@@ -110,8 +111,7 @@ def main():
     rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
     rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
     tcsc_amd.gpu_from_dense(inp["Wd"], cfg.K, ncols, csp, csn, rip, rin, stream=sh)
-    # kept for the dense baseline and the BCSR line
-    Wd = inp.pop("Wd") if (world == 1 and not (args.no_dense_baseline and args.no_bcsr)) else None
+    Wd = inp.pop("Wd")  # validation, then the dense baseline and the BCSR line
     plan = tcsc_amd.Plan.from_device(cfg.K, ncols, csp, csn, rip, rin, 0, ncols, local_rank, sh)
     plan.reserve(cfg.M)
     nnz = npos + nneg
@@ -121,6 +121,16 @@ def main():
 
     def step():
         plan.sgemm(X, B, Y, cfg.M, ncols, variant, 0.2, sh)
+
+    # ---- validation (not timed): as the reference harness validates before it
+    # measures (main.cpp:299-368), every rank checks one step's full output
+    validation = None
+    if not args.no_validate:
+        validation = validate_against_dense(tcsc_amd, cfg, ncols, variant, X, Wd, B, Y, step, sh)
+        validation["determinism"] = check_determinism(step, Y, 24)
+    if world > 1 or (args.no_dense_baseline and args.no_bcsr):
+        Wd = None
+    torch.cuda.synchronize(dev)
 
     for _ in range(args.warmup):
         step()
@@ -220,6 +230,8 @@ def main():
                 "valu_add_frac": (adds_per_launch / gather_s) / VALU_ADD_PEAK,
             },
         }
+        if validation is not None:
+            out["validation"] = validation
         if Wd is not None and not args.no_dense_baseline:
             # the reference's "TCSC vs Dense" line (main.cpp:379-391) on the
             # device -- gemm_basic's dense product with the same ternary W as an fp32 rocBLAS
@@ -264,6 +276,55 @@ def main():
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def validate_against_dense(tcsc_amd, cfg, ncols, variant, X, Wd, B, Y, step, sh):
+    """One step's full M x ncols output against the dense product of the same
+    ternary W (tcsc_gpu_dense_sgemm: fp32 rocBLAS SGEMM + the same bias/PReLU
+    epilogue), per element |y - y_dense| <= max(1, a) * 2^-19 * S with
+    S = |B| + |X| . |W| from the same dense path on magnitudes: the oracle's
+    2^-20 bound once for each of the two results.  Runs on the
+    GPU; raises (the run fails, as main.cpp exit(1)s) on a violation."""
+    import torch
+
+    a = 0.2
+    step()
+    Yd = torch.empty_like(Y)
+    tcsc_amd.dense_sgemm(X, Wd, B, Yd, cfg.M, ncols, cfg.K, ncols, variant, a, sh)
+    S = torch.empty_like(Y)
+    Xa, Wa, Ba = X.abs(), Wd.abs(), B.abs()
+    tcsc_amd.dense_sgemm(Xa, Wa, Ba, S, cfg.M, ncols, cfg.K, ncols, "basic", 0.0, sh)
+    del Xa, Wa, Ba
+    bound = S.mul_(max(1.0, a) * 2.0 ** -19)
+    err = (Y - Yd).abs_()
+    nan_mismatch = int((Y.isnan() != Yd.isnan()).sum().item())
+    ratio = torch.where(err == 0, torch.zeros_like(err), err / bound)
+    ratio = torch.nan_to_num(ratio, nan=0.0, posinf=float("inf"))
+    worst = float(ratio.max().item())
+    if nan_mismatch or not worst <= 1.0:
+        raise SystemExit(f"validation failed: worst |y - y_dense| / bound = {worst:.3g}, "
+                         f"NaN mismatches {nan_mismatch}")
+    return {"against": "dense fp32 rocBLAS SGEMM of the same ternary W (+ same epilogue)",
+            "bound": "max(1,a) * 2^-19 * (|B| + |X|.|W|) per element", "elements": Y.numel(),
+            "worst_err_over_bound": worst}
+
+
+def check_determinism(step, Y, n):
+    """The gather reduces in a fixed order (no atomics; split-K partials are
+    combined in slice order), so repeated launches must give bit-identical
+    outputs: n back-to-back launches, the last output compared bit for bit
+    with the first.  (Also lets the GPU clocks settle before the warm-up,
+    DESIGN.md §7 "clock ramp".)"""
+    import torch
+
+    step()
+    first = Y.view(torch.int32).clone()
+    for _ in range(n - 1):
+        step()
+    same = bool(torch.equal(Y.view(torch.int32), first))
+    if not same:
+        raise SystemExit(f"validation failed: output changed over {n} identical launches")
+    return {"launches": n, "bit_identical": same}
 
 
 def bcsr_line(cfg, Wd, X, B, Y, nnz, tcsc_s, timed, sh, n):
