@@ -72,6 +72,9 @@ typedef struct {
     int n_chunks;        /* ceil(K / chunk_k)                             */
     size_t device_bytes; /* HBM held by the plan                          */
     int order;           /* enum tcsc_order the plan was built for        */
+    int mfma_min_M;      /* > 0: the plan holds the MFMA image of W (near-
+                            dense W, see tcsc_gpu_sgemm) and launches with
+                            M >= mfma_min_M use it; 0: gather only        */
 } tcsc_gpu_plan_info;
 
 /* Number of HIP devices visible (0 when there is no GPU). */

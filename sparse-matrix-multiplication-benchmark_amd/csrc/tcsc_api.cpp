@@ -51,6 +51,14 @@ struct tcsc_gpu_plan {
     int order = TCSC_ORDER_FAST;
     tcsc_gpu_plan* chain_pos = nullptr;
     tcsc_gpu_plan* chain_neg = nullptr;
+    // MFMA path for near-dense W (tcsc_mfma.hip): W as three
+    // bf16 copies (3*rows x cols), and the column range's rebased CSC for the
+    // rows the bf16 split of X cannot carry.  Launches with M >= mfma_min_M
+    // take it; null when the plan is gather-only.
+    uint16_t* w3 = nullptr;
+    int *ccp = nullptr, *ccn = nullptr, *crp = nullptr, *crn = nullptr;
+    size_t mfma_bytes = 0;
+    int mfma_min_M = 0;
 };
 
 namespace {
@@ -193,13 +201,106 @@ int current_order() {
     return g_order;
 }
 
+// ---- MFMA path selection ----------------------------------
+// $TCSC_PATH at plan creation: "gather" never builds the MFMA image, "mfma"
+// builds it for any W and uses it for every M, anything else (default)
+// builds it when the density reaches kMfmaDensity and uses it for
+// M >= kMfmaMinM.  The crossover (cfg 5 measurements): the gather runs
+// ~27 T adds/s near density 0.5, the bf16 x3 GEMM ~1.7 PFLOP/s = 6 flops
+// per (m, k, n), i.e. it wins above density ~0.1; 0.2 leaves a 2x margin
+// for smaller, less efficient GEMM shapes.
+constexpr double kMfmaDensity = 0.2;
+constexpr int kMfmaMinM = 64;
+constexpr double kMfmaMaxImageBytes = 16.0 * (1ull << 30);  // 3 bf16 copies of W
+
+int path_mode() {  // 0 auto, 1 gather only, 2 mfma forced
+    const char* e = std::getenv("TCSC_PATH");
+    if (!e) return 0;
+    if (std::strcmp(e, "gather") == 0) return 1;
+    if (std::strcmp(e, "mfma") == 0) return 2;
+    return 0;
+}
+
+size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// workspace of one MFMA launch: X3 (M x 3K bf16) + M row flags + "any"
+size_t mfma_ws_bytes(int M, int K) { return align256((size_t)M * 3 * K * 2) + (size_t)(M + 1) * sizeof(int); }
+
+bool use_mfma(const tcsc_gpu_plan* p, int M) { return p->w3 && M >= p->mfma_min_M && p->rows > 0; }
+
+rocblas_handle rocblas_for_device(int dev) {
+    static std::mutex mu;
+    static std::unordered_map<int, rocblas_handle> handles;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = handles.find(dev);
+    if (it != handles.end()) return it->second;
+    rocblas_handle h = nullptr;
+    if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
+    handles[dev] = h;
+    return h;
+}
+
+void free_mfma(tcsc_gpu_plan* p) {
+    for (void* q : {(void*)p->w3, (void*)p->ccp, (void*)p->ccn, (void*)p->crp, (void*)p->crn})
+        if (q) (void)hipFree(q);
+    p->w3 = nullptr;
+    p->ccp = p->ccn = p->crp = p->crn = nullptr;
+    p->mfma_bytes = 0;
+}
+
+// Adds the MFMA image to a fast-order plan when the path mode and the density
+// call for it.  Not building it is never an error: the gather serves every M.
+int maybe_build_mfma(tcsc_gpu_plan* p, const int* csp, const int* csn, const int* rip, const int* rin, int col_begin,
+                     hipStream_t st) {
+    const int mode = path_mode();
+    const double cells = (double)p->rows * p->cols;
+    const long long nnz = p->n_pos + p->n_neg;
+    if (mode == 1 || cells == 0 || 6.0 * cells > kMfmaMaxImageBytes) return TCSC_OK;
+    if (mode == 0 && (nnz < kMfmaDensity * cells || p->rows < 64 || p->cols < 64)) return TCSC_OK;
+    const size_t n = (size_t)p->rows * p->cols;
+    DevBuf wf, bad;
+    if (wf.alloc(n * sizeof(float)) != hipSuccess || bad.alloc(sizeof(int)) != hipSuccess) {
+        (void)hipGetLastError();
+        return TCSC_OK;  // no room for the image: gather only
+    }
+    const size_t bytes = 3 * n * sizeof(uint16_t) + 2 * (size_t)(p->cols + 1) * sizeof(int) +
+                         (size_t)(p->n_pos + p->n_neg) * sizeof(int);
+    if (hipMalloc(&p->w3, 3 * n * sizeof(uint16_t)) != hipSuccess ||
+        hipMalloc(&p->ccp, (size_t)(p->cols + 1) * sizeof(int)) != hipSuccess ||
+        hipMalloc(&p->ccn, (size_t)(p->cols + 1) * sizeof(int)) != hipSuccess ||
+        hipMalloc(&p->crp, (size_t)(p->n_pos > 0 ? p->n_pos : 1) * sizeof(int)) != hipSuccess ||
+        hipMalloc(&p->crn, (size_t)(p->n_neg > 0 ? p->n_neg : 1) * sizeof(int)) != hipSuccess) {
+        (void)hipGetLastError();
+        free_mfma(p);
+        return TCSC_OK;
+    }
+    p->mfma_bytes = bytes;
+    HIP_TRY(hipMemsetAsync(bad.p, 0, sizeof(int), st));
+    HIP_TRY(tcsc::mfma_build_w3(csp, csn, rip, rin, col_begin, p->rows, p->cols, wf.as<float>(), p->w3, p->ccp,
+                                p->ccn, p->crp, p->crn, p->n_pos, p->n_neg, bad.as<int>(), st));
+    int hbad = 0;
+    HIP_TRY(hipMemcpyAsync(&hbad, bad.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (hbad) free_mfma(p);  // a column repeats a row > 256 times: not exact in bf16
+    p->mfma_min_M = mode == 2 ? 1 : kMfmaMinM;
+    return TCSC_OK;
+}
+
 // The plan, plus -- in reference order -- its two one-sign chains: the same
 // build on the same arrays with the other sign's col_start replaced by zeros.
 int build_plan_ordered(int rows, int col_begin, int ncols, long long n_pos, long long n_neg, const int* csp,
                        const int* csn, const int* rip, const int* rin, int device, hipStream_t st, int order,
                        tcsc_gpu_plan** out) {
     int rc = build_plan(rows, col_begin, ncols, n_pos, n_neg, csp, csn, rip, rin, device, st, out);
-    if (rc != TCSC_OK || order != TCSC_ORDER_REFERENCE) return rc;
+    if (rc != TCSC_OK) return rc;
+    if (order != TCSC_ORDER_REFERENCE) {
+        rc = maybe_build_mfma(*out, csp, csn, rip, rin, col_begin, st);
+        if (rc != TCSC_OK) {
+            tcsc_gpu_plan_destroy(*out);
+            *out = nullptr;
+        }
+        return rc;
+    }
     tcsc_gpu_plan* p = *out;
     p->order = order;
     DevBuf zeros;
@@ -228,6 +329,7 @@ int slices_override() {
 
 // Workspace of one call = [X^T: xt_bytes(M, K)] [split-K slabs, if any].
 size_t wanted_workspace(const tcsc_gpu_plan* p, int M) {
+    if (use_mfma(p, M)) return mfma_ws_bytes(M, p->rows);
     const int s = tcsc::choose_slices(M, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
                                       slices_override());
     return tcsc::xt_bytes(M, p->rows) + tcsc::workspace_bytes(M, p->cols, s);
@@ -331,6 +433,49 @@ class DeviceGuard {
 }  // namespace
 
 namespace {
+// The MFMA path (stage 0: all; 1: split only; 2: GEMM + epilogue on the
+// staged X3).  Y = [h|m|l] . [W;W;W] is, column-major, Y^T (cols x M, ld
+// ldy) = W3^T (cols x 3K, ld cols) . X3^T (3K x M, ld 3K).
+int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy, int variant,
+               float a, void* stream, float* ws, size_t ws_bytes, int stage) {
+    const int K = p->rows, N = p->cols;
+    const size_t need = mfma_ws_bytes(M, K);
+    if (!ws || ws_bytes < need) {
+        set_error("tcsc_gpu_sgemm: workspace of %zu bytes < %zu needed for M=%d", ws ? ws_bytes : (size_t)0, need, M);
+        return TCSC_E_ARG;
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    uint16_t* x3 = reinterpret_cast<uint16_t*>(ws);
+    int* flags = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + align256((size_t)M * 3 * K * 2));
+    int* any = flags + M;
+    if (stage != 2) HIP_TRY(tcsc::mfma_split_x(dX, M, K, x3, flags, any, st));
+    if (stage == 1) return TCSC_OK;
+    rocblas_handle h = rocblas_for_device(p->device);
+    if (!h) {
+        set_error("tcsc_gpu_sgemm: rocblas_create_handle failed");
+        return TCSC_E_HIP;
+    }
+    if (rocblas_set_stream(h, st) != rocblas_status_success) {
+        set_error("tcsc_gpu_sgemm: rocblas_set_stream failed");
+        return TCSC_E_HIP;
+    }
+    const float one = 1.0f, zero = 0.0f;
+    const rocblas_status rs =
+        rocblas_gemm_ex(h, rocblas_operation_none, rocblas_operation_none, N, M, 3 * K, &one, p->w3,
+                        rocblas_datatype_bf16_r, N, x3, rocblas_datatype_bf16_r, 3 * K, &zero, dY,
+                        rocblas_datatype_f32_r, ldy, dY, rocblas_datatype_f32_r, ldy, rocblas_datatype_f32_r,
+                        rocblas_gemm_algo_standard, 0, 0);
+    if (rs != rocblas_status_success) {
+        set_error("tcsc_gpu_sgemm: rocblas_gemm_ex failed (%s)", rocblas_status_to_string(rs));
+        return TCSC_E_HIP;
+    }
+    const bool prelu = variant >= TCSC_VARIANT_PRELU_BASIC;
+    HIP_TRY(tcsc::launch_bias_act(dY, M, N, ldy, dB, prelu, a, st));
+    HIP_TRY(tcsc::mfma_fixup(x3, M, K, p->ccp, p->ccn, p->crp, p->crn, N, dB, dY, ldy,
+                             variant == TCSC_VARIANT_BASIC, prelu, a, flags, any, st));
+    return TCSC_OK;
+}
+
 int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy, int variant,
              float a, void* stream, float* ws, size_t ws_bytes, int stage = 0) {
     if (!p || M < 0 || (stage != 1 && (ldy < p->cols || variant < 0 || variant > 4))) {
@@ -342,6 +487,7 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
         set_error("tcsc_gpu_sgemm: NULL device pointer");
         return TCSC_E_ARG;
     }
+    if (use_mfma(p, M)) return sgemm_mfma(p, dX, dB, dY, M, ldy, variant, a, stream, ws, ws_bytes, stage);
     const size_t xtb = tcsc::xt_bytes(M, p->rows);
     if (p->rows > 0 && (!ws || ws_bytes < xtb)) {
         set_error("tcsc_gpu_sgemm: workspace of %zu bytes < %zu needed for M=%d", ws ? ws_bytes : (size_t)0, xtb, M);
@@ -519,9 +665,10 @@ int tcsc_gpu_plan_get_info(const tcsc_gpu_plan* p, tcsc_gpu_plan_info* info) {
     info->n_neg = p->n_neg;
     info->chunk_k = tcsc::kTK;
     info->n_chunks = p->n_chunks;
-    info->device_bytes = p->bytes + p->ws_bytes + (p->chain_pos ? p->chain_pos->bytes : 0) +
+    info->device_bytes = p->bytes + p->ws_bytes + p->mfma_bytes + (p->chain_pos ? p->chain_pos->bytes : 0) +
                          (p->chain_neg ? p->chain_neg->bytes : 0);
     info->order = p->order;
+    info->mfma_min_M = p->w3 ? p->mfma_min_M : 0;
     return TCSC_OK;
 }
 
@@ -538,6 +685,7 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan* p) {
     if (p->ent) (void)hipFree(p->ent);
     if (p->sptr) (void)hipFree(p->sptr);
     if (p->ws) (void)hipFree(p->ws);
+    free_mfma(p);
     tcsc_gpu_plan_destroy(p->chain_pos);
     tcsc_gpu_plan_destroy(p->chain_neg);
     delete p;
@@ -548,7 +696,13 @@ int tcsc_gpu_plan_reserve(tcsc_gpu_plan* p, int max_M) {
         set_error("tcsc_gpu_plan_reserve: bad arguments");
         return TCSC_E_ARG;
     }
-    const size_t want = wanted_workspace(p, max_M);
+    // both paths' needs at max_M: a later launch with fewer rows may take the other one
+    size_t want = wanted_workspace(p, max_M);
+    if (p->w3) {
+        const int s = tcsc::choose_slices(max_M, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
+                                          slices_override());
+        want = std::max(want, tcsc::xt_bytes(max_M, p->rows) + tcsc::workspace_bytes(max_M, p->cols, s));
+    }
     if (want <= p->ws_bytes) return TCSC_OK;
     DeviceGuard dg(p->device);
     if (p->ws) {
@@ -651,21 +805,10 @@ int tcsc_gpu_dense_sgemm(const float* dX, const float* dW, const float* dB, floa
     if (M == 0 || N == 0) return TCSC_OK;
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
-    static std::mutex mu;
-    static std::unordered_map<int, rocblas_handle> handles;
-    rocblas_handle h = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        auto it = handles.find(dev);
-        if (it == handles.end()) {
-            if (rocblas_create_handle(&h) != rocblas_status_success) {
-                set_error("tcsc_gpu_dense_sgemm: rocblas_create_handle failed");
-                return TCSC_E_HIP;
-            }
-            handles[dev] = h;
-        } else {
-            h = it->second;
-        }
+    rocblas_handle h = rocblas_for_device(dev);
+    if (!h) {
+        set_error("tcsc_gpu_dense_sgemm: rocblas_create_handle failed");
+        return TCSC_E_HIP;
     }
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (rocblas_set_stream(h, st) != rocblas_status_success) {

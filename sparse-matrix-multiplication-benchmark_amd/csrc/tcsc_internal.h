@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
+#include <stdint.h>
 
 namespace tcsc {
 
@@ -154,6 +155,22 @@ hipError_t sort_columns(const int* in, int* out, int n, int ncols, const int* of
 // X (M x K) -> XT (K x ldxt), rows m >= M zero; ldxt = ldxt_for(M) (M rounded up to kTM)
 int ldxt_for(int M);
 hipError_t launch_transpose(const float* X, int M, int K, float* XT, int ldxt, hipStream_t st);
+
+// ---- MFMA path for near-dense W (tcsc_mfma.hip) ------------
+// Build: wf (rows x ncols fp32 scratch) <- the +1/-1 entries of columns
+// [col_begin, col_begin+ncols) (absolute offsets); w3 <- three bf16 copies
+// (3*rows x ncols); cp/cn (ncols+1) and crp/crn (n_pos/n_neg) <- the range's
+// rebased CSC copy.  *bad = 1 if a weight is not exact in bf16.
+hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int rows,
+                         int ncols, float* wf, uint16_t* w3, int* cp, int* cn, int* crp, int* crn, long long n_pos,
+                         long long n_neg, int* bad, hipStream_t st);
+// X (M x K) -> x3 (M x 3K bf16, [h | m | l]); flags[M] + *any (= flags + M)
+// mark the rows the fixup recomputes.
+hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int* flags, int* any, hipStream_t st);
+// Rewrites the flagged rows of Y in k_stream's fast order (no-op if *any == 0).
+hipError_t mfma_fixup(const uint16_t* x3, int M, int K, const int* cp, const int* cn, const int* crp, const int* crn,
+                      int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
+                      const int* flags, const int* any, hipStream_t st);
 
 // Error channel shared by every entry point of the library (tcsc_api.cpp):
 // the message behind tcsc_gpu_last_error(), and the host API's policy

@@ -70,6 +70,7 @@ class plan_info_t(C.Structure):
         ("device", C.c_int), ("rows", C.c_int), ("cols", C.c_int), ("col_begin", C.c_int),
         ("nnz", C.c_longlong), ("n_pos", C.c_longlong), ("n_neg", C.c_longlong),
         ("chunk_k", C.c_int), ("n_chunks", C.c_int), ("device_bytes", C.c_size_t), ("order", C.c_int),
+        ("mfma_min_M", C.c_int),
     ]
 
 

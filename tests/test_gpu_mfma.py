@@ -1,0 +1,231 @@
+"""The MFMA path for near-dense W (csrc/tcsc_mfma.hip).
+
+Plans of W with density >= 0.2 also hold W as bf16 and launches with
+M >= 64 run Y = [h|m|l] . [W;W;W] on the matrix cores (x = h + m + l split
+exactly into bf16 parts).  Same bars as the gather:
+float outputs within 2^-20 * (|b| + sum|x|) of the exact fp64 sums, integer
+inputs bit-exact with the reference's outputs for all five variants, and
+the rows the split cannot carry (inf / NaN / tiny x) recomputed in the
+gather's own order: bit-identical to the gather path.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+import tcsc_amd
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    tcsc_amd.build()
+    tcsc_amd.require_gpu()
+    tcsc_amd.set_num_shards(0)
+    return tcsc_amd.lib()
+
+
+@pytest.fixture
+def path(monkeypatch):
+    """path(mode): TCSC_PATH for plans created from now on (host-API cache dropped)."""
+
+    def set_mode(mode):
+        if mode is None:
+            monkeypatch.delenv("TCSC_PATH", raising=False)
+        else:
+            monkeypatch.setenv("TCSC_PATH", mode)
+        tcsc_amd.cache_clear()
+
+    yield set_mode
+    monkeypatch.delenv("TCSC_PATH", raising=False)
+    tcsc_amd.cache_clear()
+
+
+def device_run(W, X, B, variant, a=0.2, ldy=None, c0=0, c1=None, prepared=False):
+    import torch
+
+    dev = torch.device("cuda:0")
+    c1 = W.cols if c1 is None else c1
+    plan = tcsc_amd.Plan(W, c0, c1)
+    M, nc = X.shape[0], c1 - c0
+    ldy = ldy or nc
+    dX = torch.from_numpy(np.ascontiguousarray(X)).to(dev)
+    dB = torch.from_numpy(np.ascontiguousarray(B[c0:c1])).to(dev)
+    dY = torch.full((M, ldy), 7.0, device=dev)
+    if prepared:
+        plan.prepare_x(dX, M)
+        plan.sgemm_prepared(dB, dY, M, ldy, variant, a)
+    else:
+        plan.sgemm(dX, dB, dY, M, ldy, variant, a)
+    torch.cuda.synchronize()
+    info = plan.info()
+    plan.destroy()
+    Y = dY.cpu().numpy()
+    assert np.all(Y[:, nc:] == 7.0), "columns beyond the plan's were written"
+    return Y[:, :nc], info
+
+
+def float_case(o, M, K, N, density, seed):
+    Wd = o.ternary((K, N), density, seed)
+    return Wd, o.uniform((M, K), seed + 1), o.uniform((N,), seed + 2)
+
+
+@pytest.mark.parametrize("K", [700, 701])
+def test_float_within_bound_all_variants(gpu, oracle, path, K):
+    path(None)
+    Wd, X, B = float_case(oracle, 200, K, 300, 0.5, 31)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    Wref = oracle.tcsc_from_dense(Wd)
+    Y64, S64 = oracle.f64_rows(X, Wref, B)
+    for variant in pyoracle.VARIANTS:
+        Y, info = device_run(W, X, B, variant)
+        assert info["mfma_min_M"] == 64
+        ok, ratio = pyoracle.check_close(Y, Y64, S64, 0.2 if variant in pyoracle.PRELU_VARIANTS else None)
+        assert ok, f"{variant}: worst err/bound {ratio:.3g}"
+    W.free()
+
+
+def test_integer_inputs_bit_exact(gpu, oracle, path):
+    path(None)
+    M, K, N = 130, 512, 257
+    Wd = oracle.ternary((K, N), 0.5, 41)
+    X, B = oracle.integers((M, K), 42), oracle.integers((N,), 43)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    Wref = oracle.tcsc_from_dense(Wd)
+    for variant in pyoracle.VARIANTS:
+        Y, info = device_run(W, X, B, variant)
+        assert info["mfma_min_M"] == 64
+        ref = oracle.sgemm(variant, X, Wref, B, 0.2)
+        np.testing.assert_array_equal(Y, ref, err_msg=variant)
+        Yh = tcsc_amd.sgemm(variant, X, W, B, 0.2)  # host API: the cached plan takes the same path
+        np.testing.assert_array_equal(Yh, ref, err_msg=variant)
+    W.free()
+
+
+def test_special_rows_match_the_gather_bit_for_bit(gpu, oracle, path, monkeypatch):
+    monkeypatch.setenv("TCSC_SLICES", "1")  # the gather without split-K: one accumulator per output
+    M, K, N = 96, 256, 200
+    Wd, X, B = float_case(oracle, M, K, N, 0.4, 51)
+    X[3, 17] = np.inf
+    X[10, 0] = -np.inf
+    X[20, 100] = np.nan
+    X[30, 5] = np.float32(1e-40)   # fp32 denormal
+    X[31, 6] = np.float32(3e-35)   # normal, below 2^-100
+    X[40, :] = np.float32(1e-38)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    for variant in pyoracle.VARIANTS:
+        path(None)
+        Ym, info = device_run(W, X, B, variant)
+        assert info["mfma_min_M"] == 64
+        path("gather")
+        Yg, info = device_run(W, X, B, variant)
+        assert info["mfma_min_M"] == 0
+        flagged = [3, 10, 20, 30, 31, 40]
+        a_, b_ = Ym[flagged], Yg[flagged]
+        nan = np.isnan(b_)
+        assert nan.any() and np.array_equal(np.isnan(a_), nan), variant
+        np.testing.assert_array_equal(a_[~nan].view(np.uint32), b_[~nan].view(np.uint32), err_msg=variant)
+        rest = np.setdiff1d(np.arange(M), flagged)
+        assert np.isfinite(Ym[rest]).all()
+        Y64, S64 = oracle.f64_rows(X[rest], oracle.tcsc_from_dense(Wd), B)
+        ok, ratio = pyoracle.check_close(Ym[rest], Y64, S64, 0.2 if variant in pyoracle.PRELU_VARIANTS else None)
+        assert ok, f"{variant}: worst err/bound {ratio:.3g}"
+    W.free()
+
+
+def test_path_modes_and_small_M(gpu, oracle, path):
+    Wd, X, B = float_case(oracle, 100, 300, 128, 0.05, 61)  # sparse: auto builds no MFMA image
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    Wref = oracle.tcsc_from_dense(Wd)
+    path(None)
+    assert device_run(W, X, B, "basic")[1]["mfma_min_M"] == 0
+    path("mfma")  # forced: any density, any M
+    for M in (1, 5, 100):
+        Y, info = device_run(W, X[:M], B, "prelu_onthego")
+        assert info["mfma_min_M"] == 1
+        Y64, S64 = oracle.f64_rows(X[:M], Wref, B)
+        assert pyoracle.check_close(Y, Y64, S64, 0.2)[0]
+    W.free()
+    # dense W, M below the threshold: the gather serves it
+    path(None)
+    Wd2, X2, B2 = float_case(oracle, 40, 300, 128, 0.6, 62)
+    W2 = tcsc_amd.TcscMatrix.from_dense(Wd2)
+    Y, info = device_run(W2, X2, B2, "basic")
+    assert info["mfma_min_M"] == 64
+    Y64, S64 = oracle.f64_rows(X2, oracle.tcsc_from_dense(Wd2), B2)
+    assert pyoracle.check_close(Y, Y64, S64)[0]
+    W2.free()
+
+
+def test_column_block_pitch_and_prepared(gpu, oracle, path):
+    path(None)
+    Wd, X, B = float_case(oracle, 256, 512, 400, 0.5, 71)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    Wref = oracle.tcsc_from_dense(Wd)
+    Y64, S64 = oracle.f64_rows(X, Wref, B)
+    for c0, c1, ldy in ((0, 400, 403), (96, 333, 240), (250, 400, 150)):
+        for prepared in (False, True):
+            Y, info = device_run(W, X, B, "prelu_separate", c0=c0, c1=c1, ldy=ldy, prepared=prepared)
+            assert info["mfma_min_M"] == 64
+            ok, ratio = pyoracle.check_close(Y, Y64[:, c0:c1], S64[:, c0:c1], 0.2)
+            assert ok, f"[{c0},{c1}) ldy={ldy} prepared={prepared}: {ratio:.3g}"
+    W.free()
+
+
+def test_repeated_rows_in_a_column(gpu, oracle, path):
+    """A hand-built TCSC whose columns repeat rows (within a sign and across
+    signs): every entry counts, as in the reference's loops (tcsc.c:86-93)."""
+    path(None)
+    K, N, M = 80, 70, 100
+    rng = np.random.default_rng(5)
+    cols_p, cols_n = [], []
+    for j in range(N):
+        p = np.sort(rng.integers(0, K, 40))  # repeats likely
+        n = np.sort(rng.integers(0, K, 30))
+        cols_p.append(p)
+        cols_n.append(n)
+    csp = np.concatenate([[0], np.cumsum([len(c) for c in cols_p])]).astype(np.int32)
+    csn = np.concatenate([[0], np.cumsum([len(c) for c in cols_n])]).astype(np.int32)
+    rip = np.concatenate(cols_p).astype(np.int32)
+    rin = np.concatenate(cols_n).astype(np.int32)
+    W = tcsc_amd.TcscMatrix.from_arrays(K, N, csp, csn, rip, rin)
+    Wref = pyoracle.TCSC(K, N, csp, csn, rip, rin)
+    X, B = oracle.integers((M, K), 81), oracle.integers((N,), 82)
+    Y, info = device_run(W, X, B, "basic")
+    assert info["mfma_min_M"] == 64
+    np.testing.assert_array_equal(Y, oracle.sgemm("basic", X, Wref, B))
+    W.free()
+
+
+def test_baseline_cfg5_sampled_rows(gpu, oracle, path):
+    """BASELINE cfg 5 (M=2048, K=N=8192, 50 %) through the device API takes
+    the MFMA path; sampled rows against the exact fp64 sums."""
+    import torch
+
+    from tcsc_amd import workloads
+
+    path(None)
+    cfg = workloads.CONFIGS[5]
+    dev = torch.device("cuda:0")
+    inp = workloads.make_device_inputs(cfg, 0, cfg.N, dev)
+    K, N = cfg.K, cfg.N
+    csp = torch.empty(N + 1, dtype=torch.int32, device=dev)
+    csn = torch.empty(N + 1, dtype=torch.int32, device=dev)
+    npos, nneg = tcsc_amd.gpu_from_dense(inp["Wd"], K, N, csp, csn)
+    rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
+    rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
+    tcsc_amd.gpu_from_dense(inp["Wd"], K, N, csp, csn, rip, rin)
+    del inp["Wd"]
+    plan = tcsc_amd.Plan.from_device(K, N, csp, csn, rip, rin)
+    assert plan.info()["mfma_min_M"] == 64
+    Y = torch.empty((cfg.M, N), device=dev)
+    plan.sgemm(inp["X"], inp["B"], Y, cfg.M, N, "basic", 0.2)
+    torch.cuda.synchronize()
+    rows = np.unique(np.concatenate([[0, cfg.M - 1], np.random.default_rng(5).integers(0, cfg.M, 6)]))
+    W = pyoracle.TCSC(K, N, csp.cpu().numpy(), csn.cpu().numpy(), rip[:npos].cpu().numpy(), rin[:nneg].cpu().numpy())
+    Y64, S64 = oracle.f64_rows(inp["X"][torch.from_numpy(rows).to(dev)].cpu().numpy(), W, inp["B"].cpu().numpy())
+    ok, ratio = pyoracle.check_close(Y[torch.from_numpy(rows).to(dev)].cpu().numpy(), Y64, S64)
+    assert ok, f"worst err/bound {ratio:.3g}"
+    plan.destroy()
