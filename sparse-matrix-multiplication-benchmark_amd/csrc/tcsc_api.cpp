@@ -51,8 +51,8 @@ struct tcsc_gpu_plan {
     int order = TCSC_ORDER_FAST;
     tcsc_gpu_plan* chain_pos = nullptr;
     tcsc_gpu_plan* chain_neg = nullptr;
-    // MFMA path for near-dense W (tcsc_mfma.hip): W as three
-    // bf16 copies (3*rows x cols), and the column range's rebased CSC for the
+    // MFMA path for near-dense W (tcsc_mfma.hip): W^T with
+    // three bf16 copies per column (cols x 3*rows), and the column range's rebased CSC for the
     // rows the bf16 split of X cannot carry.  Launches with M >= mfma_min_M
     // take it; null when the plan is gather-only.
     uint16_t* w3 = nullptr;
@@ -435,7 +435,8 @@ class DeviceGuard {
 namespace {
 // The MFMA path (stage 0: all; 1: split only; 2: GEMM + epilogue on the
 // staged X3).  Y = [h|m|l] . [W;W;W] is, column-major, Y^T (cols x M, ld
-// ldy) = W3^T (cols x 3K, ld cols) . X3^T (3K x M, ld 3K).
+// ldy) = op_T(W3T) (cols x 3K; W3T stored 3K-contiguous per column) .
+// X3^T (3K x M, ld 3K).
 int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy, int variant,
                float a, void* stream, float* ws, size_t ws_bytes, int stage) {
     const int K = p->rows, N = p->cols;
@@ -461,8 +462,8 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
     }
     const float one = 1.0f, zero = 0.0f;
     const rocblas_status rs =
-        rocblas_gemm_ex(h, rocblas_operation_none, rocblas_operation_none, N, M, 3 * K, &one, p->w3,
-                        rocblas_datatype_bf16_r, N, x3, rocblas_datatype_bf16_r, 3 * K, &zero, dY,
+        rocblas_gemm_ex(h, rocblas_operation_transpose, rocblas_operation_none, N, M, 3 * K, &one, p->w3,
+                        rocblas_datatype_bf16_r, 3 * K, x3, rocblas_datatype_bf16_r, 3 * K, &zero, dY,
                         rocblas_datatype_f32_r, ldy, dY, rocblas_datatype_f32_r, ldy, rocblas_datatype_f32_r,
                         rocblas_gemm_algo_standard, 0, 0);
     if (rs != rocblas_status_success) {

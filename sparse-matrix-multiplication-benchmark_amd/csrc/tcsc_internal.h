@@ -157,9 +157,9 @@ int ldxt_for(int M);
 hipError_t launch_transpose(const float* X, int M, int K, float* XT, int ldxt, hipStream_t st);
 
 // ---- MFMA path for near-dense W (tcsc_mfma.hip) ------------
-// Build: wf (rows x ncols fp32 scratch) <- the +1/-1 entries of columns
-// [col_begin, col_begin+ncols) (absolute offsets); w3 <- three bf16 copies
-// (3*rows x ncols); cp/cn (ncols+1) and crp/crn (n_pos/n_neg) <- the range's
+// Build: wf (ncols x rows fp32 scratch) <- the +1/-1 entries of columns
+// [col_begin, col_begin+ncols) (absolute offsets), transposed; w3 <- W^T
+// with three bf16 copies per row (ncols x 3*rows); cp/cn (ncols+1) and crp/crn (n_pos/n_neg) <- the range's
 // rebased CSC copy.  *bad = 1 if a weight is not exact in bf16.
 hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int rows,
                          int ncols, float* wf, uint16_t* w3, int* cp, int* cn, int* crp, int* crn, long long n_pos,

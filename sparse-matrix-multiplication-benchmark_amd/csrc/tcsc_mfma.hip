@@ -8,6 +8,7 @@
 // 8 + 8 + 8 significand bits), W is exact in bf16 (0, +-1, or small
 // integers for duplicate rows), so each product is exact and the GEMM
 //     Y = [h | m | l] . [W ; W ; W]           (M x 3K) . (3K x N)
+// (W stored transposed, N x 3K, so both operands run along k)
 // accumulates in fp32 on the matrix cores (rocBLAS gemm_ex bf16 -> f32).
 // Only the summation order differs from the gather's: the result is within
 // the fast-order bound, and bit-exact on integer-valued inputs.
@@ -102,30 +103,36 @@ __global__ void k_split3(const float* __restrict__ X, int M, int K, uint16_t* __
     }
 }
 
-// The +1/-1 entries of column j (rebased CSC, rows ascending) added into a
-// dense fp32 K x ncols image (atomics: a row may repeat in a column).
+// The +1/-1 entries of column j (rebased CSC) added into a dense fp32 image
+// of W^T (ncols x K, k contiguous; atomics: a row may repeat in a column).
 __global__ void k_w_scatter(const int* __restrict__ cs, const int* __restrict__ ri, int col_begin, int ncols,
-                            float sign, float* __restrict__ Wf) {
+                            int K, float sign, float* __restrict__ WfT) {
     const int lane = threadIdx.x & 63;
     const int j = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (j >= ncols) return;
     const int base = cs[col_begin];
     const int e0 = cs[col_begin + j] - base, e1 = cs[col_begin + j + 1] - base;
     const int* r = ri + base;
-    for (int e = e0 + lane; e < e1; e += 64) atomicAdd(&Wf[(size_t)r[e] * ncols + j], sign);
+    for (int e = e0 + lane; e < e1; e += 64) atomicAdd(&WfT[(size_t)j * K + r[e]], sign);
 }
 
-// Wf (K x ncols fp32) -> W3 (3K x ncols bf16: three copies).  Values must be
-// integers of magnitude <= 256 to be exact in bf16; *bad = 1 otherwise.
-__global__ void k_w3_from(const float* __restrict__ Wf, long long n, uint16_t* __restrict__ W3, int* __restrict__ bad) {
+// WfT (ncols x K fp32) -> W3T (ncols x 3K bf16): row n = [w | w | w], so both
+// GEMM operands run along k (the "TN" form, ~8 % faster than W3 as 3K x
+// ncols: tools/dense3_bench.cpp).  Values must be integers of magnitude
+// <= 256 to be exact in bf16; *bad = 1 otherwise.
+__global__ void k_w3_from(const float* __restrict__ WfT, int ncols, int K, uint16_t* __restrict__ W3T,
+                          int* __restrict__ bad) {
+    const long long n = (long long)ncols * K;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
          i += (long long)gridDim.x * blockDim.x) {
-        const float w = Wf[i];
+        const float w = WfT[i];
         if (fabsf(w) > 256.0f) *bad = 1;
         const uint16_t b = (uint16_t)(f2u(w) >> 16);
-        W3[i] = b;
-        W3[n + i] = b;
-        W3[2 * n + i] = b;
+        const long long j = i / K, k = i - j * K;
+        uint16_t* row = W3T + j * 3 * K;
+        row[k] = b;
+        row[K + k] = b;
+        row[2 * K + k] = b;
     }
 }
 
@@ -183,11 +190,11 @@ hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const i
     const int wpb = 4;  // waves (columns) per block
     if (n_pos > 0)
         hipLaunchKernelGGL(k_w_scatter, dim3((ncols + wpb - 1) / wpb), dim3(64 * wpb), 0, st, csp, rip, col_begin,
-                           ncols, 1.0f, wf);
+                           ncols, rows, 1.0f, wf);
     if (n_neg > 0)
         hipLaunchKernelGGL(k_w_scatter, dim3((ncols + wpb - 1) / wpb), dim3(64 * wpb), 0, st, csn, rin, col_begin,
-                           ncols, -1.0f, wf);
-    hipLaunchKernelGGL(k_w3_from, dim3(grid_of(n, 256)), dim3(256), 0, st, wf, n, w3, bad);
+                           ncols, rows, -1.0f, wf);
+    hipLaunchKernelGGL(k_w3_from, dim3(grid_of(n, 256)), dim3(256), 0, st, wf, ncols, rows, w3, bad);
     if ((e = rebase_offsets(csp, col_begin, ncols, cp, st)) != hipSuccess) return e;
     if ((e = rebase_offsets(csn, col_begin, ncols, cn, st)) != hipSuccess) return e;
     if (n_pos > 0)

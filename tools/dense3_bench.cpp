@@ -9,6 +9,8 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <vector>
 
 #define HIPOK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 #define RBOK(x) do { rocblas_status s = (x); if (s != rocblas_status_success) { printf("rocBLAS %s @%d\n", rocblas_status_to_string(s), __LINE__); exit(1);} } while (0)
@@ -39,8 +41,17 @@ int main(int argc, char** argv) {
     HIPOK(hipMalloc(&C, (size_t)M * N * 4));
     HIPOK(hipMalloc(&A32, (size_t)M * K * 4));
     HIPOK(hipMalloc(&B32, (size_t)K * N * 4));
-    HIPOK(hipMemset(A, 0, (size_t)M * 3 * K * 2));
-    HIPOK(hipMemset(B, 0, (size_t)3 * K * N * 2));
+    {   // realistic operands (zeros run the matrix cores at lower power): X parts
+        // ~U[-1,1) bf16, W ternary at 50 %
+        std::vector<uint16_t> h((size_t)3 * K * N);
+        unsigned long long s = 88172645463325252ull;
+        auto rnd = [&] { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
+        for (auto& v : h) { const unsigned r = rnd() & 3; v = r == 0 ? 0x3f80 : r == 1 ? 0xbf80 : 0; }
+        HIPOK(hipMemcpy(B, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+        h.resize((size_t)M * 3 * K);
+        for (auto& v : h) { float f = (float)((rnd() >> 11) * (1.0 / 9007199254740992.0)) * 2 - 1; unsigned u; memcpy(&u, &f, 4); v = u >> 16; }
+        HIPOK(hipMemcpy(A, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    }
     HIPOK(hipMemset(A32, 0, (size_t)M * K * 4));
     HIPOK(hipMemset(B32, 0, (size_t)K * N * 4));
     const float one = 1.f, zero = 0.f;
@@ -53,7 +64,15 @@ int main(int argc, char** argv) {
                                  rocblas_datatype_f32_r, N, C, rocblas_datatype_f32_r, N, rocblas_datatype_f32_r,
                                  rocblas_gemm_algo_standard, 0, 0));
         }, 10);
-        printf("bf16 x%d (K'=%d) -> f32: %.3f ms  (%.0f TFLOP/s)\n", parts, KK, ms, 2.0 * M * KK * (double)N / ms * 1e-9);
+        printf("NN bf16 x%d (K'=%d) -> f32: %.3f ms  (%.0f TFLOP/s)\n", parts, KK, ms, 2.0 * M * KK * (double)N / ms * 1e-9);
+        // TN: W stored N x K' (k contiguous), both operands K-contiguous
+        const float ms2 = time_ms([&] {
+            RBOK(rocblas_gemm_ex(h, rocblas_operation_transpose, rocblas_operation_none, N, M, KK, &one, B,
+                                 rocblas_datatype_bf16_r, KK, A, rocblas_datatype_bf16_r, KK, &zero, C,
+                                 rocblas_datatype_f32_r, N, C, rocblas_datatype_f32_r, N, rocblas_datatype_f32_r,
+                                 rocblas_gemm_algo_standard, 0, 0));
+        }, 10);
+        printf("TN bf16 x%d (K'=%d) -> f32: %.3f ms  (%.0f TFLOP/s)\n", parts, KK, ms2, 2.0 * M * KK * (double)N / ms2 * 1e-9);
     }
     const float ms32 = time_ms([&] {
         RBOK(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, N, M, K, &one, (float*)B32, N,

@@ -17,7 +17,12 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_dispatch(root, counter, kernel="k_stream"):
+# the fast-order prelu_basic instantiation bench.py times (k_stream<BIAS_FIRST,
+# PRELU, OUT, ORDER>); the reference-order lines of the same run are ORDER 1/2
+KERNEL = os.environ.get("TRAFFIC_KERNEL", "k_stream<false, true, 0, 0>")
+
+
+def per_dispatch(root, counter, kernel=KERNEL):
     vals = collections.defaultdict(float)
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -38,7 +43,7 @@ def main():
     f_kib = sum(fetch) / len(fetch)
     w_kib = sum(write) / len(write)
     rec = {
-        "kernel": "k_stream",
+        "kernel": KERNEL,
         "fetch_size_kib_raw": f_kib,
         "write_size_kib": w_kib,
         "hbm_bytes_per_launch": (2.0 * f_kib + w_kib) * 1024.0,
