@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--no-bcsr", action="store_true", help="skip the BCSR (1x8 blocks) line (N=1 only)")
     p.add_argument("--no-reference-order", action="store_true",
                    help="skip the reference-summation-order line (N=1 only)")
+    p.add_argument("--no-other-configs", action="store_true",
+                   help="skip the other BASELINE configs' timings (N=1 only)")
     p.add_argument("--no-validate", action="store_true", help="skip the pre-timing check against the dense product")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
     p.add_argument("--override", default="", help="experiments only: e.g. 'K=16448,N=4096' (marks the line)")
@@ -270,12 +272,58 @@ def main():
                 ref[v] = {"ms": t * 1e3, "g_add_ops_per_s": adds_per_launch / t / 1e9, "vs_fast_order": t / gather_s}
             rplan.destroy()
             out["reference_order"] = ref
+        if world == 1 and not args.no_other_configs and not args.override:
+            out["other_configs"] = other_configs(tcsc_amd, workloads, dev, sh, timed, cfg.idx)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, cfg, variant, X, B, csp, csn, rip[:npos], rin[:nneg])
         print(json.dumps(out), flush=True)
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def other_configs(tcsc_amd, workloads, dev, sh, timed, skip):
+    """The other BASELINE configs on this GPU (not part of `value`): one full
+    tcsc_gpu_sgemm per step (X staging + gather, or split + GEMM on the MFMA
+    path for near-dense W), inputs resident, HIP events over 30 launches
+    after 10 warm-up launches."""
+    import torch
+
+    res = {}
+    for idx in (2, 3, 5):
+        if idx == skip:
+            continue
+        c = workloads.CONFIGS[idx]
+        inp = workloads.make_device_inputs(c, 0, c.N, dev)
+        csp = torch.empty(c.N + 1, dtype=torch.int32, device=dev)
+        csn = torch.empty(c.N + 1, dtype=torch.int32, device=dev)
+        npos, nneg = tcsc_amd.gpu_from_dense(inp["Wd"], c.K, c.N, csp, csn, stream=sh)
+        rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
+        rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
+        tcsc_amd.gpu_from_dense(inp["Wd"], c.K, c.N, csp, csn, rip, rin, stream=sh)
+        del inp["Wd"]
+        plan = tcsc_amd.Plan.from_device(c.K, c.N, csp, csn, rip, rin, 0, c.N, dev.index or 0, sh)
+        plan.reserve(c.M)
+        mfma_min = plan.info()["mfma_min_M"]
+        Yc = torch.empty((c.M, c.N), device=dev)
+
+        def one():
+            plan.sgemm(inp["X"], inp["B"], Yc, c.M, c.N, c.variant, 0.2, sh)
+
+        for _ in range(10):
+            one()
+        t = timed(one, 30)
+        nnz = npos + nneg
+        res[c.name] = {
+            "workload": c.describe(), "variant": c.variant, "nnz": nnz, "ms": t * 1e3,
+            "g_add_ops_per_s": workloads.add_ops(c.M, nnz, c.N) / t / 1e9,
+            "hbm_frac": workloads.algorithmic_bytes(c.M, c.K, c.N, nnz) / t / (HBM_PEAK_GBS * 1e9),
+            "path": "mfma (bf16 x3 split GEMM)" if mfma_min and c.M >= mfma_min else "gather (k_stream)",
+        }
+        plan.destroy()
+        del inp, csp, csn, rip, rin, Yc
+    torch.cuda.empty_cache()
+    return res
 
 
 def validate_against_dense(tcsc_amd, cfg, ncols, variant, X, Wd, B, Y, step, sh):
