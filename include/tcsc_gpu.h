@@ -126,7 +126,14 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan *plan);
  *        otherwise.
  * Asynchronous on `stream`; once the workspace covers M (see
  * tcsc_gpu_plan_reserve) no allocation and no synchronisation (safe to
- * capture in a hipGraph). */
+ * capture in a hipGraph).
+ * Near-dense W (density >= 0.2, see tcsc_gpu_plan_info.mfma_min_M): launches
+ * with M >= mfma_min_M run the MFMA path -- X split exactly into three bf16
+ * parts and one rocBLAS bf16 GEMM with fp32 accumulation against the plan's
+ * bf16 image of W -- with the same accuracy bounds as the gather (DESIGN.md
+ * §4).  rocBLAS may allocate on its first call on a device: make one launch
+ * before capturing such a plan.  $TCSC_PATH=gather|mfma at plan creation
+ * disables / forces the path. */
 int tcsc_gpu_sgemm(const tcsc_gpu_plan *plan, const float *dX, const float *dB,
                    float *dY, int M, int ldy, int variant, float a,
                    void *stream);
