@@ -683,6 +683,50 @@ __global__ void k_reduce(const float* __restrict__ ws, int slices, int M, int nc
     }
 }
 
+// The same with 4 columns per thread (16-B slab loads, all slices' loads in
+// flight before the adds); same order per element, so the same bits.  Needs
+// ncols % 4 == 0, ldy % 4 == 0 and 16-B aligned ws, Y.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+template <bool BIAS_FIRST, bool PRELU>
+__global__ void k_reduce4(const f32x4_t* __restrict__ ws, int slices, int M, int ncols,
+                          const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a) {
+    const int nq = ncols / 4;
+    const long long total = (long long)M * nq;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int row = (int)(i / nq), col = 4 * (int)(i % nq);
+        f32x4_t p[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+            if (s < slices) p[s] = __builtin_nontemporal_load(ws + (size_t)s * total + i);
+        const float4 b = *reinterpret_cast<const float4*>(Bias + col);
+        float4 v = BIAS_FIRST ? b : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+            if (s < slices) {
+                v.x += p[s].x;
+                v.y += p[s].y;
+                v.z += p[s].z;
+                v.w += p[s].w;
+            }
+        if (!BIAS_FIRST) {
+            v.x += b.x;
+            v.y += b.y;
+            v.z += b.z;
+            v.w += b.w;
+        }
+        if (PRELU) {
+            v.x = (v.x < 0.0f) ? a * v.x : v.x;
+            v.y = (v.y < 0.0f) ? a * v.y : v.y;
+            v.z = (v.z < 0.0f) ? a * v.z : v.z;
+            v.w = (v.w < 0.0f) ? a * v.w : v.w;
+        }
+        typedef float nt4 __attribute__((ext_vector_type(4)));
+        nt4 w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<nt4*>(Y + (size_t)row * ldy + col));
+    }
+}
+
 // Dense-baseline epilogue (gemm_basic order, dense/dense.c:64-77: the bias
 // after the sum): Y = act(Y + B), one float4 of a row per thread where the
 // row pitch allows, HBM-bound (2*M*N*4 bytes).
@@ -884,8 +928,15 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const long long total = (long long)g.M * g.ncols;
-    hipLaunchKernelGGL((k_reduce<BF, PR>), dim3(grid_for(total, 256)), dim3(256), 0, st, g.ws, slices, g.M,
-                       g.ncols, g.B, g.Y, g.ldy, g.a);
+    const bool vec = slices <= 16 && g.ncols % 4 == 0 && g.ldy % 4 == 0 &&
+                     ((reinterpret_cast<uintptr_t>(g.Y) | reinterpret_cast<uintptr_t>(g.ws) |
+                       reinterpret_cast<uintptr_t>(g.B)) & 15) == 0;
+    if (vec)
+        hipLaunchKernelGGL((k_reduce4<BF, PR>), dim3(grid_for(total / 4, 256)), dim3(256), 0, st,
+                           reinterpret_cast<const f32x4_t*>(g.ws), slices, g.M, g.ncols, g.B, g.Y, g.ldy, g.a);
+    else
+        hipLaunchKernelGGL((k_reduce<BF, PR>), dim3(grid_for(total, 256)), dim3(256), 0, st, g.ws, slices, g.M,
+                           g.ncols, g.B, g.Y, g.ldy, g.a);
     return hipGetLastError();
 }
 
