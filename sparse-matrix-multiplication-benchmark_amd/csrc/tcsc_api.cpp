@@ -11,6 +11,7 @@
 // unless TCSC_ON_ERROR=continue -- aborts, because silently leaving Y
 // unwritten would be worse than the reference's behaviour.
 #include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt.h>
 #include <rocblas/rocblas.h>
 
 #include <algorithm>
@@ -29,6 +30,16 @@
 #include "../../include/sparse/tcsc.h"
 #include "../../include/tcsc_gpu.h"
 #include "tcsc_internal.h"
+
+// One hipBLASLt GEMM of the MFMA path (a launch shape of one plan): the
+// matmul descriptor, the three layouts and the algorithm the heuristic chose.
+struct LtGemm {
+    int M = 0, ldy = 0, bias = 0;
+    hipblasLtMatmulDesc_t desc = nullptr;
+    hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+    hipblasLtMatmulAlgo_t algo{};
+    bool ok = false;
+};
 
 struct tcsc_gpu_plan {
     int device = 0;
@@ -59,6 +70,7 @@ struct tcsc_gpu_plan {
     int *ccp = nullptr, *ccn = nullptr, *crp = nullptr, *crn = nullptr;
     size_t mfma_bytes = 0;
     int mfma_min_M = 0;
+    std::vector<LtGemm> lt;  // hipBLASLt setups per (M, ldy, bias epilogue), made on first use
 };
 
 namespace {
@@ -240,7 +252,81 @@ rocblas_handle rocblas_for_device(int dev) {
     return h;
 }
 
+hipblasLtHandle_t lt_for_device(int dev) {
+    static std::mutex mu;
+    static std::unordered_map<int, hipblasLtHandle_t> handles;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = handles.find(dev);
+    if (it != handles.end()) return it->second;
+    hipblasLtHandle_t h = nullptr;
+    if (hipblasLtCreate(&h) != HIPBLAS_STATUS_SUCCESS) return nullptr;
+    handles[dev] = h;
+    return h;
+}
+
+void free_lt(LtGemm& g) {
+    if (g.la) (void)hipblasLtMatrixLayoutDestroy(g.la);
+    if (g.lb) (void)hipblasLtMatrixLayoutDestroy(g.lb);
+    if (g.lc) (void)hipblasLtMatrixLayoutDestroy(g.lc);
+    if (g.desc) (void)hipblasLtMatmulDescDestroy(g.desc);
+    g = LtGemm{};
+}
+
+// The MFMA path's GEMM as hipBLASLt sees it: D (cols x M, ld ldy, f32) =
+// op_T(W3T) (3K x cols bf16, k contiguous) . X3^T (3K x M bf16), fp32
+// accumulation, optionally + bias (the BIAS epilogue: bias added after the
+// sum, as the gather's bias-last variants).  The first launch of a shape asks
+// the heuristic for its best workspace-free algorithm (tools/hblt_bench.cpp:
+// ~10 % faster than rocBLAS gemm_ex's pick at cfg 5, and the epilogue saves
+// the separate bias pass); ok = false sends the launch to rocBLAS.
+LtGemm* lt_gemm_for(tcsc_gpu_plan* p, int M, int ldy, bool bias) {
+    for (auto& g : p->lt)
+        if (g.M == M && g.ldy == ldy && g.bias == (int)bias) return &g;
+    const char* force = std::getenv("TCSC_MFMA_GEMM");  // "rocblas": A/B against rocBLAS gemm_ex
+    hipblasLtHandle_t h = (force && std::strcmp(force, "rocblas") == 0) ? nullptr : lt_for_device(p->device);
+    LtGemm g;
+    g.M = M;
+    g.ldy = ldy;
+    g.bias = bias;
+    const int KK = 3 * p->rows, N = p->cols;
+    const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
+    const hipblasLtEpilogue_t epi = bias ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT;
+    const hipDataType bt = HIP_R_32F;
+    const uint64_t no_ws = 0;
+    hipblasLtMatmulPreference_t pref = nullptr;
+    hipblasLtMatmulHeuristicResult_t res{};
+    int n = 0;
+    g.ok = h && hipblasLtMatmulDescCreate(&g.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) == HIPBLAS_STATUS_SUCCESS &&
+           hipblasLtMatmulDescSetAttribute(g.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof ta) == HIPBLAS_STATUS_SUCCESS &&
+           hipblasLtMatmulDescSetAttribute(g.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof tb) == HIPBLAS_STATUS_SUCCESS &&
+           hipblasLtMatmulDescSetAttribute(g.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof epi) == HIPBLAS_STATUS_SUCCESS &&
+           (!bias || hipblasLtMatmulDescSetAttribute(g.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof bt) ==
+                         HIPBLAS_STATUS_SUCCESS) &&
+           hipblasLtMatrixLayoutCreate(&g.la, HIP_R_16BF, KK, N, KK) == HIPBLAS_STATUS_SUCCESS &&
+           hipblasLtMatrixLayoutCreate(&g.lb, HIP_R_16BF, KK, M, KK) == HIPBLAS_STATUS_SUCCESS &&
+           hipblasLtMatrixLayoutCreate(&g.lc, HIP_R_32F, N, M, ldy) == HIPBLAS_STATUS_SUCCESS &&
+           hipblasLtMatmulPreferenceCreate(&pref) == HIPBLAS_STATUS_SUCCESS &&
+           hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &no_ws,
+                                                 sizeof no_ws) == HIPBLAS_STATUS_SUCCESS &&
+           hipblasLtMatmulAlgoGetHeuristic(h, g.desc, g.la, g.lb, g.lc, g.lc, pref, 1, &res, &n) ==
+               HIPBLAS_STATUS_SUCCESS &&
+           n > 0 && res.state == HIPBLAS_STATUS_SUCCESS;
+    if (pref) (void)hipblasLtMatmulPreferenceDestroy(pref);
+    if (g.ok) {
+        g.algo = res.algo;
+    } else {
+        free_lt(g);
+        g.M = M;
+        g.ldy = ldy;
+        g.bias = bias;
+    }
+    p->lt.push_back(g);
+    return &p->lt.back();
+}
+
 void free_mfma(tcsc_gpu_plan* p) {
+    for (auto& g : p->lt) free_lt(g);
+    p->lt.clear();
     for (void* q : {(void*)p->w3, (void*)p->ccp, (void*)p->ccn, (void*)p->crp, (void*)p->crn})
         if (q) (void)hipFree(q);
     p->w3 = nullptr;
@@ -451,27 +537,41 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
     int* any = flags + M;
     if (stage != 2) HIP_TRY(tcsc::mfma_split_x(dX, M, K, x3, flags, any, st));
     if (stage == 1) return TCSC_OK;
-    rocblas_handle h = rocblas_for_device(p->device);
-    if (!h) {
-        set_error("tcsc_gpu_sgemm: rocblas_create_handle failed");
-        return TCSC_E_HIP;
-    }
-    if (rocblas_set_stream(h, st) != rocblas_status_success) {
-        set_error("tcsc_gpu_sgemm: rocblas_set_stream failed");
-        return TCSC_E_HIP;
-    }
     const float one = 1.0f, zero = 0.0f;
-    const rocblas_status rs =
-        rocblas_gemm_ex(h, rocblas_operation_transpose, rocblas_operation_none, N, M, 3 * K, &one, p->w3,
-                        rocblas_datatype_bf16_r, 3 * K, x3, rocblas_datatype_bf16_r, 3 * K, &zero, dY,
-                        rocblas_datatype_f32_r, ldy, dY, rocblas_datatype_f32_r, ldy, rocblas_datatype_f32_r,
-                        rocblas_gemm_algo_standard, 0, 0);
-    if (rs != rocblas_status_success) {
-        set_error("tcsc_gpu_sgemm: rocblas_gemm_ex failed (%s)", rocblas_status_to_string(rs));
-        return TCSC_E_HIP;
-    }
     const bool prelu = variant >= TCSC_VARIANT_PRELU_BASIC;
-    HIP_TRY(tcsc::launch_bias_act(dY, M, N, ldy, dB, prelu, a, st));
+    // hipBLASLt, with the bias in its epilogue unless a PReLU pass follows anyway
+    LtGemm* g = lt_gemm_for(const_cast<tcsc_gpu_plan*>(p), M, ldy, !prelu);
+    bool bias_done = false;
+    if (g->ok) {
+        if (g->bias && hipblasLtMatmulDescSetAttribute(g->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &dB,
+                                                       sizeof dB) != HIPBLAS_STATUS_SUCCESS) {
+            set_error("tcsc_gpu_sgemm: hipBLASLt bias pointer");
+            return TCSC_E_HIP;
+        }
+        const hipblasStatus_t ls = hipblasLtMatmul(lt_for_device(p->device), g->desc, &one, p->w3, g->la, x3, g->lb,
+                                                   &zero, dY, g->lc, dY, g->lc, &g->algo, nullptr, 0, st);
+        if (ls != HIPBLAS_STATUS_SUCCESS) {
+            set_error("tcsc_gpu_sgemm: hipblasLtMatmul failed (%d)", (int)ls);
+            return TCSC_E_HIP;
+        }
+        bias_done = g->bias;
+    } else {
+        rocblas_handle h = rocblas_for_device(p->device);
+        if (!h || rocblas_set_stream(h, st) != rocblas_status_success) {
+            set_error("tcsc_gpu_sgemm: no rocBLAS handle");
+            return TCSC_E_HIP;
+        }
+        const rocblas_status rs =
+            rocblas_gemm_ex(h, rocblas_operation_transpose, rocblas_operation_none, N, M, 3 * K, &one, p->w3,
+                            rocblas_datatype_bf16_r, 3 * K, x3, rocblas_datatype_bf16_r, 3 * K, &zero, dY,
+                            rocblas_datatype_f32_r, ldy, dY, rocblas_datatype_f32_r, ldy, rocblas_datatype_f32_r,
+                            rocblas_gemm_algo_standard, 0, 0);
+        if (rs != rocblas_status_success) {
+            set_error("tcsc_gpu_sgemm: rocblas_gemm_ex failed (%s)", rocblas_status_to_string(rs));
+            return TCSC_E_HIP;
+        }
+    }
+    if (!bias_done) HIP_TRY(tcsc::launch_bias_act(dY, M, N, ldy, dB, prelu, a, st));
     HIP_TRY(tcsc::mfma_fixup(x3, M, K, p->ccp, p->ccn, p->crp, p->crn, N, dB, dY, ldy,
                              variant == TCSC_VARIANT_BASIC, prelu, a, flags, any, st));
     return TCSC_OK;
