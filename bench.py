@@ -11,7 +11,9 @@ K=N=16384, 98 % sparse, PReLU) -- the configuration the north star's target
 is quoted on.  With N ranks each GPU owns one column block:
   --scaling weak   (default) every rank owns a full 16384-column block of a
                    N*16384-column W (per-GPU work fixed as N grows);
-  --scaling strong the cfg4 matrix itself is split into N column blocks.
+  --scaling strong the cfg4 matrix itself is split over the N ranks: into column
+                   blocks (--shard cols, X replicated) or row blocks (--shard rows:
+                   each rank stages only its rows of X; W is replicated).
 There is no collective on the data path; the only collectives are the
 timing barrier and the max-over-ranks of the elapsed time.
 
@@ -48,6 +50,8 @@ def parse():
     p.add_argument("--config", type=int, default=4)
     p.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     p.add_argument("--variant", default=None, help="override the config's variant")
+    p.add_argument("--shard", choices=("cols", "rows"), default="cols",
+                   help="strong scaling / --shard-of: split N (X replicated) or M (X split, W replicated)")
     p.add_argument("--shard-of", type=int, default=0,
                    help="time only rank 0's block of an S-way strong split (per-GPU view of S GPUs)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -93,14 +97,23 @@ def main():
         kv = dict(x.split("=") for x in args.override.split(","))
         cfg = dataclasses.replace(cfg, **{k: (float(v) if k == "sparsity" else int(v)) for k, v in kv.items()})
     variant = args.variant or cfg.variant
-    # this rank's column block
+    # this rank's block: all rows x a column block (--shard cols), or a row
+    # block x all columns (--shard rows: X split instead of replicated)
+    cfg_full = cfg
+    r0, r1 = 0, cfg.M
     if args.scaling == "weak":
         c0, c1, seed_off = 0, cfg.N, rank
     else:
-        c0, c1 = column_range(cfg.N, world, rank)
-        seed_off = 0
+        c0, c1, seed_off = 0, cfg.N, 0
+        if args.shard == "cols":
+            c0, c1 = column_range(cfg.N, world, rank)
+        else:
+            r0, r1 = column_range(cfg.M, world, rank)
     if args.shard_of > 1:
-        c0, c1 = column_range(cfg.N, args.shard_of, 0)
+        if args.shard == "cols":
+            c0, c1 = column_range(cfg.N, args.shard_of, 0)
+        else:
+            r0, r1 = column_range(cfg.M, args.shard_of, 0)
     ncols = c1 - c0
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
@@ -114,6 +127,11 @@ def main():
     rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
     tcsc_amd.gpu_from_dense(inp["Wd"], cfg.K, ncols, csp, csn, rip, rin, stream=sh)
     Wd = inp.pop("Wd")  # validation, then the dense baseline and the BCSR line
+    if (r0, r1) != (0, cfg.M):  # a row block: the same X on every rank, this rank's rows
+        import dataclasses
+
+        inp["X"] = inp["X"][r0:r1].contiguous()
+        cfg = dataclasses.replace(cfg, M=r1 - r0)
     plan = tcsc_amd.Plan.from_device(cfg.K, ncols, csp, csn, rip, rin, 0, ncols, local_rank, sh)
     plan.reserve(cfg.M)
     nnz = npos + nneg
@@ -211,10 +229,15 @@ def main():
             "dtype": "f32",
             "data": "synthetic (X,B ~ U[-1,1), W iid ternary; seeded torch generators)",
             "config": {
-                "workload": f"{cfg.name}: {cfg.describe()}" + (f" [override {args.override}]" if args.override else ""),
-                "M": cfg.M, "K": cfg.K, "N": cfg.N, "sparsity": cfg.sparsity, "variant": variant,
+                "workload": f"{cfg_full.name}: {cfg_full.describe()}"
+                            + (f" [override {args.override}]" if args.override else ""),
+                "M": cfg_full.M, "K": cfg.K, "N": cfg.N, "sparsity": cfg.sparsity, "variant": variant,
                 "columns_per_gpu": ncols, "nnz_per_gpu": nnz,
-                "parallelism": f"column-shard x{world} ({args.scaling}), no collective",
+                "parallelism": (f"per-GPU view: rank 0's block of a {args.shard_of}-way {args.shard} split"
+                                if args.shard_of > 1 else
+                                f"{'row' if args.shard == 'rows' and args.scaling == 'strong' else 'column'}"
+                                f"-shard x{world} ({args.scaling}), no collective"),
+                "rows_per_gpu": cfg.M,
             },
             "roofline": {
                 "bound": "hbm",
