@@ -1,4 +1,4 @@
-"""Multi-rank column sharding on CPU (gloo, world_size 2 and 3): each rank
+"""Multi-rank column (and row) sharding on CPU (gloo, world_size 2 and 3): each rank
 takes its column block (tcsc_amd.shard.column_range), slices W/B exactly as
 the GPU ranks do, computes its block with the oracle, and the gathered blocks
 must equal the single-process result bit for bit.  No collective is used for
@@ -21,6 +21,48 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def _row_worker(rank, world, port, q):
+    """bench.py --scaling strong --shard rows: rank r stages rows
+    column_range(M, world, r) of X (the same X everywhere) against the whole W."""
+    import sys
+
+    sys.path.insert(0, PKG_DIR_FOR_WORKERS)
+    sys.path.insert(0, ORACLE_DIR_FOR_WORKERS)
+    import pyoracle
+    from tcsc_amd.shard import all_ranges, column_range
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        o = pyoracle.load_oracle()
+        M, K, N = 23, 300, 64
+        X = o.uniform((M, K), 4)
+        Wd = o.ternary((K, N), 0.1, 5)
+        B = o.uniform((N,), 6)
+        W = o.tcsc_from_dense(Wd)
+        r0, r1 = column_range(M, world, rank)
+        Yb = o.sgemm("prelu_onthego", np.ascontiguousarray(X[r0:r1]), W, B, 0.2)
+        hmax = max(b - a for a, b in all_ranges(M, world))
+        buf = torch.zeros((hmax, N), dtype=torch.float32)
+        buf[: r1 - r0] = torch.from_numpy(Yb)
+        outs = [torch.zeros_like(buf) for _ in range(world)]
+        dist.all_gather(outs, buf)
+        if rank == 0:
+            Y = np.concatenate([outs[r][: b - a].numpy() for r, (a, b) in enumerate(all_ranges(M, world))], 0)
+            q.put(bool(np.array_equal(Y, o.sgemm("prelu_onthego", X, W, B, 0.2))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_shards_concat_to_full(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_row_worker, args=(world, _free_port(), q), nprocs=world, join=True, start_method="spawn")
+    assert q.get(timeout=60)
 
 
 def _worker(rank, world, port, q):
