@@ -938,12 +938,25 @@ int tcsc_gpu_dense_sgemm(const float* dX, const float* dW, const float* dB, floa
 // ===========================================================================
 namespace {
 
-// One column block of W on one device.
+// One column block of W on one device (column axis), or one device's plan of
+// the whole W (row axis: the calls split M over the devices instead).
 struct Shard {
     int device = 0;
     int c0 = 0, c1 = 0;
     tcsc_gpu_plan* plan = nullptr;
 };
+
+// How the host API spreads a call over the GPUs ($TCSC_SHARD_AXIS, read when
+// a tcsc_t is first cached).  rows (default): block s of S owns rows
+// [M*s/S, M*(s+1)/S) of X and Y and uses its device's plan of the whole W --
+// each device receives only its rows of X over PCIe.  cols: block s owns the
+// columns [N*s/S, N*(s+1)/S) of W, B and Y, and every device receives all
+// of X.  Either way no data moves between the GPUs.
+enum { kAxisRows = 0, kAxisCols = 1 };
+int shard_axis() {
+    const char* e = std::getenv("TCSC_SHARD_AXIS");
+    return (e && std::strcmp(e, "cols") == 0) ? kAxisCols : kAxisRows;
+}
 
 struct CacheEntry {
     // fingerprint: the shape, the array addresses and a hash of the array
@@ -954,7 +967,9 @@ struct CacheEntry {
     const int *csp = nullptr, *csn = nullptr, *rip = nullptr, *rin = nullptr;
     uint64_t content = 0;
     int order = TCSC_ORDER_FAST;  // the summation order the shards' plans were built for
-    std::vector<Shard> shards;
+    int axis = kAxisRows;         // shard_axis() when built
+    int blocks = 1;               // S: row or column blocks per call
+    std::vector<Shard> shards;    // cols: one per column block; rows: one per device used
 };
 
 // Per-device staging buffers for X, B and Y of the host API.
@@ -977,7 +992,8 @@ void destroy_entry(CacheEntry& e) {
 bool fingerprint_matches(const CacheEntry& e, const tcsc_t* W, uint64_t content) {
     return e.rows == W->rows && e.cols == W->cols && e.n_pos == W->n_elem_pos && e.n_neg == W->n_elem_neg &&
            e.csp == W->col_start_pos && e.csn == W->col_start_neg && e.rip == W->row_index_pos &&
-           e.rin == W->row_index_neg && e.content == content && e.order == current_order();
+           e.rin == W->row_index_neg && e.content == content && e.order == current_order() &&
+           e.axis == shard_axis();
 }
 
 [[noreturn]] void die() {
@@ -1044,14 +1060,17 @@ int get_entry_locked(const tcsc_t* W, CacheEntry** out) {
     e.rin = W->row_index_neg;
     e.content = content;
     e.order = current_order();
+    e.axis = shard_axis();
     int S = num_shards_locked(ndev);
-    if (S > W->cols && W->cols > 0) S = W->cols;
+    if (e.axis == kAxisCols && S > W->cols && W->cols > 0) S = W->cols;
     if (S < 1) S = 1;
-    for (int s = 0; s < S; ++s) {
+    e.blocks = S;
+    const int nplans = e.axis == kAxisRows ? std::min(S, ndev) : S;
+    for (int s = 0; s < nplans; ++s) {
         Shard sh;
         sh.device = s % ndev;
-        sh.c0 = (int)((long long)W->cols * s / S);
-        sh.c1 = (int)((long long)W->cols * (s + 1) / S);
+        sh.c0 = e.axis == kAxisRows ? 0 : (int)((long long)W->cols * s / S);
+        sh.c1 = e.axis == kAxisRows ? W->cols : (int)((long long)W->cols * (s + 1) / S);
         DevState& ds = g_dev[sh.device];
         {
             DeviceGuard dg(sh.device);
@@ -1069,20 +1088,32 @@ int get_entry_locked(const tcsc_t* W, CacheEntry** out) {
     return TCSC_OK;
 }
 
-// Everything one device does for one call: H2D X once, then per shard:
-// H2D bias slice, launch, D2H of the M x (c1-c0) block into Y's columns.
-int run_device(int dev, const std::vector<const Shard*>& shards, const float* X, const float* B, float* Y,
-               int M, int N, int K, int variant, float a) {
+// One block of a call: rows [m0, m1) x the plan's columns [c0, c1).
+struct Job {
+    const Shard* sh;
+    int m0, m1;
+};
+
+// Everything one device does for one call, job by job: H2D of the job's rows
+// of X (skipped when the previous job staged the same rows), H2D of the bias
+// slice, the launch, D2H of the (m1-m0) x (c1-c0) block into Y.
+int run_device(int dev, const std::vector<Job>& jobs, const float* X, const float* B, float* Y, int N, int K,
+               int variant, float a) {
     DeviceGuard dg(dev);
     DevState& ds = g_dev[dev];
     hipStream_t st = ds.stream;
-    const size_t xb = (size_t)M * K * sizeof(float);
-    int rc;
-    if ((rc = ensure(&ds.x, &ds.x_cap, xb)) != TCSC_OK) return rc;
-    if (xb) HIP_TRY(hipMemcpyAsync(ds.x, X, xb, hipMemcpyHostToDevice, st));
-    for (const Shard* sh : shards) {
-        const int nc = sh->c1 - sh->c0;
-        if (nc == 0) continue;
+    int rc, staged0 = -1, staged1 = -1;
+    for (const Job& j : jobs) {
+        const Shard* sh = j.sh;
+        const int nc = sh->c1 - sh->c0, M = j.m1 - j.m0;
+        if (nc == 0 || M == 0) continue;
+        if (j.m0 != staged0 || j.m1 != staged1) {
+            const size_t xb = (size_t)M * K * sizeof(float);
+            if ((rc = ensure(&ds.x, &ds.x_cap, xb)) != TCSC_OK) return rc;
+            if (xb) HIP_TRY(hipMemcpyAsync(ds.x, X + (size_t)j.m0 * K, xb, hipMemcpyHostToDevice, st));
+            staged0 = j.m0;
+            staged1 = j.m1;
+        }
         if ((rc = ensure(&ds.b, &ds.b_cap, (size_t)nc * sizeof(float))) != TCSC_OK) return rc;
         if ((rc = ensure(&ds.y, &ds.y_cap, (size_t)M * nc * sizeof(float))) != TCSC_OK) return rc;
         const size_t wsb = wanted_workspace(sh->plan, M);
@@ -1090,8 +1121,9 @@ int run_device(int dev, const std::vector<const Shard*>& shards, const float* X,
         HIP_TRY(hipMemcpyAsync(ds.b, B + sh->c0, (size_t)nc * sizeof(float), hipMemcpyHostToDevice, st));
         if ((rc = sgemm_ws(sh->plan, ds.x, ds.b, ds.y, M, nc, variant, a, st, ds.ws, ds.ws_cap)) != TCSC_OK)
             return rc;
-        HIP_TRY(hipMemcpy2DAsync(Y + sh->c0, (size_t)N * sizeof(float), ds.y, (size_t)nc * sizeof(float),
-                                 (size_t)nc * sizeof(float), M, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpy2DAsync(Y + (size_t)j.m0 * N + sh->c0, (size_t)N * sizeof(float), ds.y,
+                                 (size_t)nc * sizeof(float), (size_t)nc * sizeof(float), M, hipMemcpyDeviceToHost,
+                                 st));
         HIP_TRY(hipStreamSynchronize(st));
     }
     HIP_TRY(hipStreamSynchronize(st));
@@ -1114,21 +1146,29 @@ void host_sgemm(int variant, const float* X, const tcsc_t* W, const float* B, fl
         report(rc);
         return;
     }
-    // group shards by device
-    std::vector<std::vector<const Shard*>> per_dev(g_dev.size());
-    for (const auto& s : e->shards) per_dev[s.device].push_back(&s);
+    // the call's blocks, grouped by device
+    std::vector<std::vector<Job>> per_dev(g_dev.size());
+    if (e->axis == kAxisRows) {
+        const int S = e->blocks, P = (int)e->shards.size();
+        for (int s = 0; s < S; ++s) {
+            const Shard* sh = &e->shards[s % P];
+            per_dev[sh->device].push_back(Job{sh, (int)((long long)M * s / S), (int)((long long)M * (s + 1) / S)});
+        }
+    } else {
+        for (const auto& s : e->shards) per_dev[s.device].push_back(Job{&s, 0, M});
+    }
     std::vector<int> used;
     for (size_t d = 0; d < per_dev.size(); ++d)
         if (!per_dev[d].empty()) used.push_back((int)d);
     if (used.size() == 1) {
-        rc = run_device(used[0], per_dev[used[0]], X, B, Y, M, N, K, variant, a);
+        rc = run_device(used[0], per_dev[used[0]], X, B, Y, N, K, variant, a);
     } else {
         std::vector<int> rcs(used.size(), TCSC_OK);
         std::vector<std::string> errs(used.size());
         std::vector<std::thread> th;
         for (size_t i = 0; i < used.size(); ++i)
             th.emplace_back([&, i] {
-                rcs[i] = run_device(used[i], per_dev[used[i]], X, B, Y, M, N, K, variant, a);
+                rcs[i] = run_device(used[i], per_dev[used[i]], X, B, Y, N, K, variant, a);
                 if (rcs[i] != TCSC_OK) errs[i] = g_last_error;  // thread-local
             });
         for (auto& t : th) t.join();

@@ -158,10 +158,13 @@ def test_prepare_then_gather_equals_sgemm(gpu, torch_cuda, name):
     plan.destroy()
 
 
+@pytest.mark.parametrize("axis", ["rows", "cols"])
 @pytest.mark.parametrize("shards", [2, 3, 5])
-def test_multi_shard_host_path_equals_single(gpu, shards):
-    """The column-block path (one block per GPU on a node; several blocks
-    per device here) concatenates to the single-block result bit for bit."""
+def test_multi_shard_host_path_equals_single(gpu, shards, axis, monkeypatch):
+    """The host API's blocks (one per GPU on a node; several per device here)
+    concatenate to the single-block result bit for bit: row blocks
+    (TCSC_SHARD_AXIS=rows, the default) and column blocks."""
+    monkeypatch.setenv("TCSC_SHARD_AXIS", axis)
     g = load_golden("grid_m16_k512_n1024_nz8")
     W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
     tcsc_amd.set_num_shards(1)
@@ -172,6 +175,31 @@ def test_multi_shard_host_path_equals_single(gpu, shards):
     finally:
         tcsc_amd.set_num_shards(0)
     np.testing.assert_array_equal(Ys, Y1)
+    W.free()
+
+
+@pytest.mark.parametrize("axis", ["rows", "cols"])
+def test_multi_shard_host_path_large(gpu, oracle, axis, monkeypatch):
+    """Row blocks of a launch-sized problem (each block its own launch on the
+    same plan) against the exact sums, and against one block on integers."""
+    monkeypatch.setenv("TCSC_SHARD_AXIS", axis)
+    M, K, N = 1000, 1500, 700
+    Wd = oracle.ternary((K, N), 0.05, 91)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    Wref = oracle.tcsc_from_dense(Wd)
+    X, B = oracle.uniform((M, K), 92), oracle.uniform((N,), 93)
+    Xi, Bi = oracle.integers((M, K), 94), oracle.integers((N,), 95)
+    tcsc_amd.set_num_shards(3)
+    try:
+        Y = tcsc_amd.sgemm("basic", X, W, B)
+        Yi = tcsc_amd.sgemm("prelu_basic", Xi, W, Bi, 0.2)
+    finally:
+        tcsc_amd.set_num_shards(0)
+    Y64, S64 = oracle.f64_rows(X, Wref, B)
+    ok, ratio = pyoracle.check_close(Y, Y64, S64)
+    assert ok, f"worst err/bound {ratio:.3g}"
+    np.testing.assert_array_equal(Yi, oracle.sgemm("prelu_basic", Xi, Wref, Bi, 0.2))
+    W.free()
 
 
 def test_device_plan_from_device_arrays_and_gpu_builder(gpu, torch_cuda, oracle):
