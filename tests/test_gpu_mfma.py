@@ -15,6 +15,7 @@ import pytest
 
 import pyoracle
 import tcsc_amd
+from conftest import GOLDEN_NAMES, load_golden, tcsc_of
 
 pytestmark = pytest.mark.gpu
 
@@ -229,3 +230,52 @@ def test_baseline_cfg5_sampled_rows(gpu, oracle, path):
     ok, ratio = pyoracle.check_close(Y[torch.from_numpy(rows).to(dev)].cpu().numpy(), Y64, S64)
     assert ok, f"worst err/bound {ratio:.3g}"
     plan.destroy()
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_golden_fixtures_forced_mfma(gpu, oracle, path, name):
+    """Every golden fixture (made by the reference's own tcsc.c) through the
+    MFMA path (TCSC_PATH=mfma: any density, any M): integer fixtures bit for
+    bit, float fixtures within the bound, the specials fixture with the same
+    NaN / inf classification (its rows go through the fixup)."""
+    path("mfma")
+    g = load_golden(name)
+    W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
+    kind, a = g["meta"]["kind"], float(g["a"])
+    for variant in pyoracle.VARIANTS:
+        Y = tcsc_amd.sgemm(variant, g["X"], W, g["B"], a)
+        ref = g["Y_" + variant]
+        if kind == "int":
+            np.testing.assert_array_equal(Y.view(np.uint32), ref.view(np.uint32), err_msg=variant)
+        elif kind == "special":
+            assert np.array_equal(np.isnan(Y), np.isnan(ref)), variant
+            assert np.array_equal(np.isinf(Y), np.isinf(ref)), variant
+            fin = np.isfinite(ref)
+            np.testing.assert_allclose(Y[fin], ref[fin], rtol=0, atol=1e-5)
+        else:
+            Y64, S64 = oracle.f64_rows(g["X"], tcsc_of(g), g["B"])
+            ok, ratio = pyoracle.check_close(Y, Y64, S64, a if variant in pyoracle.PRELU_VARIANTS else None)
+            assert ok, f"{variant}: worst err/bound {ratio:.3g}"
+    W.free()
+
+
+def test_reference_order_never_takes_the_mfma_path(gpu, oracle, path):
+    """TCSC_ORDER_REFERENCE plans keep the gather (the reference's order is a
+    sequence of fp32 adds a GEMM cannot reproduce): a near-dense W with
+    M >= 64 stays bit-identical to the oracle's restatement of tcsc.c."""
+    path(None)
+    Wd, X, B = float_case(oracle, 128, 300, 96, 0.5, 101)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    Wref = oracle.tcsc_from_dense(Wd)
+    tcsc_amd.set_order("reference")
+    tcsc_amd.cache_clear()
+    try:
+        for variant in pyoracle.VARIANTS:
+            Y, info = device_run(W, X, B, variant)
+            assert info["mfma_min_M"] == 0 and info["order"] == 1
+            ref = oracle.sgemm(variant, X, Wref, B, 0.2)
+            np.testing.assert_array_equal(Y.view(np.uint32), ref.view(np.uint32), err_msg=variant)
+    finally:
+        tcsc_amd.set_order("fast")
+        tcsc_amd.cache_clear()
+    W.free()
