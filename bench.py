@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--no-bcsr", action="store_true", help="skip the BCSR (1x8 blocks) line (N=1 only)")
     p.add_argument("--no-reference-order", action="store_true",
                    help="skip the reference-summation-order line (N=1 only)")
+    p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                   help="nccl (= RCCL, one GPU per rank); gloo lets ranks share a GPU (rehearsal only)")
     p.add_argument("--no-other-configs", action="store_true",
                    help="skip the other BASELINE configs' timings (N=1 only)")
     p.add_argument("--no-validate", action="store_true", help="skip the pre-timing check against the dense product")
@@ -82,10 +84,18 @@ def main():
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 needs one process per GPU: launch with torchrun --nproc-per-node N")
     distributed = world > 1
+    # one GPU per rank; with --dist-backend gloo several ranks may share a GPU
+    # (a rehearsal of the multi-rank path on a one-GPU box: RCCL refuses that)
+    ndev = torch.cuda.device_count()  # does not initialise the GPU
+    gpu = local_rank if args.dist_backend == "nccl" or ndev == 0 else local_rank % ndev
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    local_rank = gpu
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     tcsc_amd.require_gpu()
@@ -192,7 +202,8 @@ def main():
     gather_s = timed(lambda: plan.sgemm_prepared(B, Y, cfg.M, ncols, variant, 0.2, sh), nsplit)
 
     ops_rank = workloads.add_ops(cfg.M, nnz, ncols) * args.steps
-    stats = torch.tensor([elapsed, float(ops_rank)], dtype=torch.float64, device=dev)
+    stats = torch.tensor([elapsed, float(ops_rank)], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
     if distributed:
         t_max = stats[:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
