@@ -440,32 +440,42 @@ def bcsr_line(cfg, Wd, X, B, Y, nnz, tcsc_s, timed, sh, n):
 
 
 def cpu_baseline(args, cfg, variant, X, B, csp, csn, rip, rin):
-    """Oracle (C restatement of tcsc_sgemm_prelu_basic, 1 core; and the
-    OpenMP sparseGEMM_PReLU restatement on all cores) on row blocks of the
-    same workload until ~cpu_seconds of CPU work are spent."""
+    """The reference's own tcsc_sgemm_* (sparse/tcsc.c compiled in place into
+    oracle/_ref, IEEE flags) on 1 core when that build is present, else the
+    oracle's C restatement of it; the restatement on 1 core as well; and the
+    OpenMP sparseGEMM_PReLU restatement on all cores.  Row blocks of the same
+    workload until ~cpu_seconds of CPU work are spent (split between the two
+    1-core legs)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
 
     import pyoracle
 
     o = pyoracle.load_oracle()
+    ref = pyoracle.load_reference()
     ncols = csp.numel() - 1
     W = pyoracle.TCSC(cfg.K, ncols, csp.cpu().numpy(), csn.cpu().numpy(), rip.cpu().numpy(), rin.cpu().numpy())
     Bh = B.cpu().numpy()
     nnz = W.nnz
-    # 1 core, scalar port of the reference's loop (tcsc.c:143-165)
-    rows_per_block = 16
-    done, t0 = 0, time.perf_counter()
-    budget = args.cpu_seconds
-    while done < cfg.M:
-        r1 = min(cfg.M, done + rows_per_block)
-        Xs = X[done:r1].cpu().numpy()
-        o.sgemm(variant if variant in pyoracle.VARIANTS else "prelu_basic", Xs, W, Bh, 0.2)
-        done = r1
-        if time.perf_counter() - t0 > budget:
-            break
-    t1 = time.perf_counter() - t0
-    v1 = (done * nnz + done * ncols) / t1 / 1e9
+    var = variant if variant in pyoracle.VARIANTS else "prelu_basic"
+
+    def one_core(fn, rows_per_block, budget):
+        # 1 core, row blocks of the reference's loop (tcsc.c:143-165)
+        done, t0 = 0, time.perf_counter()
+        while done < cfg.M:
+            r1 = min(cfg.M, done + rows_per_block)
+            fn(var, X[done:r1].cpu().numpy(), W, Bh, 0.2)
+            done = r1
+            if time.perf_counter() - t0 > budget:
+                break
+        t = time.perf_counter() - t0
+        return done, t, (done * nnz + done * ncols) / t / 1e9
+
+    budget = args.cpu_seconds / (2 if ref else 1)
+    # Reference.sgemm copies W's arrays per call: blocks of 128 rows keep that under ~3 %
+    ref_leg = one_core(ref.sgemm, 128, budget) if ref else None
+    done, t1, v_port = one_core(o.sgemm, 16, budget)
+    v1 = ref_leg[2] if ref else v_port
     # all host cores (OpenMP, SparseGEMM.h:151-168 order)
     threads = min(os.cpu_count() or 1, 16)
     rows = min(cfg.M, max(64, done * threads))
@@ -474,17 +484,23 @@ def cpu_baseline(args, cfg, variant, X, B, csp, csn, rip, rin):
     o.sparse_gemm_omp(Xs, W, Bh, prelu=True, a=0.2, threads=threads)
     t2 = time.perf_counter() - t2
     vomp = (rows * nnz + rows * ncols) / t2 / 1e9
-    return {
+    out = {
         "value": v1,
         "unit": "G-add-ops/s",
         "cores": 1,
-        "kind": "port",
-        "sample": f"{cfg.name}: first {done} of {cfg.M} rows x all {ncols} columns, {variant} "
-                  f"(oracle/tcsc_oracle.c, gcc -O2), {t1:.1f} s",
+        "kind": "reference" if ref else "port",
+        "sample": (f"{cfg.name}: first {ref_leg[0]} of {cfg.M} rows x all {ncols} columns, {var} "
+                   f"(the reference's sparse/tcsc.c compiled in place, g++ -O2 IEEE: oracle/Makefile), "
+                   f"{ref_leg[1]:.1f} s") if ref else
+                  (f"{cfg.name}: first {done} of {cfg.M} rows x all {ncols} columns, {var} "
+                   f"(oracle/tcsc_oracle.c, gcc -O2), {t1:.1f} s"),
+        "port_value": v_port,
+        "port_sample": f"first {done} rows, oracle/tcsc_oracle.c restatement, {t1:.1f} s",
         "omp_value": vomp,
         "omp_cores": threads,
         "omp_sample": f"first {rows} rows, oracle_sparse_gemm_omp ({threads} threads), {t2:.1f} s",
     }
+    return out
 
 
 if __name__ == "__main__":
