@@ -67,8 +67,11 @@ struct tcsc_gpu_plan {
     // rows the bf16 split of X cannot carry.  Launches with M >= mfma_min_M
     // take it; null when the plan is gather-only.
     uint16_t* w3 = nullptr;
-    int *ccp = nullptr, *ccn = nullptr, *crp = nullptr, *crn = nullptr;
     size_t mfma_bytes = 0;
+    // the column range's rebased CSC (fast-order plans): the small-M path
+    // walks it, the MFMA path's fixup recomputes flagged rows from it
+    int *ccp = nullptr, *ccn = nullptr, *crp = nullptr, *crn = nullptr;
+    size_t csc_bytes = 0;
     int mfma_min_M = 0;
     std::vector<LtGemm> lt;  // hipBLASLt setups per (M, ldy, bias epilogue), made on first use
 };
@@ -327,11 +330,57 @@ LtGemm* lt_gemm_for(tcsc_gpu_plan* p, int M, int ldy, bool bias) {
 void free_mfma(tcsc_gpu_plan* p) {
     for (auto& g : p->lt) free_lt(g);
     p->lt.clear();
-    for (void* q : {(void*)p->w3, (void*)p->ccp, (void*)p->ccn, (void*)p->crp, (void*)p->crn})
-        if (q) (void)hipFree(q);
+    if (p->w3) (void)hipFree(p->w3);
     p->w3 = nullptr;
-    p->ccp = p->ccn = p->crp = p->crn = nullptr;
     p->mfma_bytes = 0;
+}
+
+void free_csc(tcsc_gpu_plan* p) {
+    for (void* q : {(void*)p->ccp, (void*)p->ccn, (void*)p->crp, (void*)p->crn})
+        if (q) (void)hipFree(q);
+    p->ccp = p->ccn = p->crp = p->crn = nullptr;
+    p->csc_bytes = 0;
+}
+
+// The rebased CSC copy of a fast-order plan's column range (4 bytes per
+// nonzero + 8 per column).  Not building it is not an error: the small-M
+// path and the MFMA path are then off for this plan.
+int build_csc(tcsc_gpu_plan* p, const int* csp, const int* csn, const int* rip, const int* rin, int col_begin,
+              hipStream_t st) {
+    if (p->cols == 0) return TCSC_OK;
+    if (hipMalloc(&p->ccp, (size_t)(p->cols + 1) * sizeof(int)) != hipSuccess ||
+        hipMalloc(&p->ccn, (size_t)(p->cols + 1) * sizeof(int)) != hipSuccess ||
+        hipMalloc(&p->crp, (size_t)(p->n_pos > 0 ? p->n_pos : 1) * sizeof(int)) != hipSuccess ||
+        hipMalloc(&p->crn, (size_t)(p->n_neg > 0 ? p->n_neg : 1) * sizeof(int)) != hipSuccess) {
+        (void)hipGetLastError();
+        free_csc(p);
+        return TCSC_OK;
+    }
+    p->csc_bytes = 2 * (size_t)(p->cols + 1) * sizeof(int) + (size_t)(p->n_pos + p->n_neg) * sizeof(int);
+    HIP_TRY(tcsc::csc_copy(csp, csn, rip, rin, col_begin, p->cols, p->n_pos, p->n_neg, p->ccp, p->ccn, p->crp,
+                           p->crn, st));
+    return TCSC_OK;
+}
+
+// Small-M path (tcsc_small.hip) on fast-order plans.  It costs ~3 ps per
+// (nonzero, row) at cfg 4's shape (X gathers from L2, one wave per column);
+// the gather costs the same ~256-row tile for any M <= 256 (~0.06 ps per
+// (nonzero, row) of the tile, plus ~20 us of staging and launch).  So: every
+// M <= 4, and M <= 16 while M * nnz <= 2^24 (launch overhead dominates).
+// Measured on one box (tools/small_m.sh): 1 x 512 x 2048 6.5 vs 33.8 us,
+// 4 x 16384^2 (98 %) 62 vs 99 us, 16 x 4096^2 (95 %) 25 vs 34 us,
+// 16 x 16384^2 260 vs 100 us (there the gather stays).  $TCSC_SMALL_M caps M
+// (0 = off).
+constexpr int kSmallMaxM = 16;
+int small_max_m() {
+    const char* e = std::getenv("TCSC_SMALL_M");
+    if (!e) return kSmallMaxM;
+    return std::max(0, std::min(kSmallMaxM, std::atoi(e)));
+}
+
+bool use_small(const tcsc_gpu_plan* p, int M) {
+    if (!p->ccp || p->rows <= 0 || M < 1 || M > small_max_m() || use_mfma(p, M)) return false;
+    return M <= 4 || (double)M * (double)(p->n_pos + p->n_neg) <= 16777216.0;
 }
 
 // Adds the MFMA image to a fast-order plan when the path mode and the density
@@ -343,27 +392,22 @@ int maybe_build_mfma(tcsc_gpu_plan* p, const int* csp, const int* csn, const int
     const long long nnz = p->n_pos + p->n_neg;
     if (mode == 1 || cells == 0 || 6.0 * cells > kMfmaMaxImageBytes) return TCSC_OK;
     if (mode == 0 && (nnz < kMfmaDensity * cells || p->rows < 64 || p->cols < 64)) return TCSC_OK;
+    if (!p->ccp) return TCSC_OK;  // the fixup needs the CSC copy
     const size_t n = (size_t)p->rows * p->cols;
     DevBuf wf, bad;
     if (wf.alloc(n * sizeof(float)) != hipSuccess || bad.alloc(sizeof(int)) != hipSuccess) {
         (void)hipGetLastError();
         return TCSC_OK;  // no room for the image: gather only
     }
-    const size_t bytes = 3 * n * sizeof(uint16_t) + 2 * (size_t)(p->cols + 1) * sizeof(int) +
-                         (size_t)(p->n_pos + p->n_neg) * sizeof(int);
-    if (hipMalloc(&p->w3, 3 * n * sizeof(uint16_t)) != hipSuccess ||
-        hipMalloc(&p->ccp, (size_t)(p->cols + 1) * sizeof(int)) != hipSuccess ||
-        hipMalloc(&p->ccn, (size_t)(p->cols + 1) * sizeof(int)) != hipSuccess ||
-        hipMalloc(&p->crp, (size_t)(p->n_pos > 0 ? p->n_pos : 1) * sizeof(int)) != hipSuccess ||
-        hipMalloc(&p->crn, (size_t)(p->n_neg > 0 ? p->n_neg : 1) * sizeof(int)) != hipSuccess) {
+    if (hipMalloc(&p->w3, 3 * n * sizeof(uint16_t)) != hipSuccess) {
         (void)hipGetLastError();
         free_mfma(p);
         return TCSC_OK;
     }
-    p->mfma_bytes = bytes;
+    p->mfma_bytes = 3 * n * sizeof(uint16_t);
     HIP_TRY(hipMemsetAsync(bad.p, 0, sizeof(int), st));
-    HIP_TRY(tcsc::mfma_build_w3(csp, csn, rip, rin, col_begin, p->rows, p->cols, wf.as<float>(), p->w3, p->ccp,
-                                p->ccn, p->crp, p->crn, p->n_pos, p->n_neg, bad.as<int>(), st));
+    HIP_TRY(tcsc::mfma_build_w3(csp, csn, rip, rin, col_begin, p->rows, p->cols, wf.as<float>(), p->w3, p->n_pos,
+                                p->n_neg, bad.as<int>(), st));
     int hbad = 0;
     HIP_TRY(hipMemcpyAsync(&hbad, bad.p, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -380,7 +424,8 @@ int build_plan_ordered(int rows, int col_begin, int ncols, long long n_pos, long
     int rc = build_plan(rows, col_begin, ncols, n_pos, n_neg, csp, csn, rip, rin, device, st, out);
     if (rc != TCSC_OK) return rc;
     if (order != TCSC_ORDER_REFERENCE) {
-        rc = maybe_build_mfma(*out, csp, csn, rip, rin, col_begin, st);
+        rc = build_csc(*out, csp, csn, rip, rin, col_begin, st);
+        if (rc == TCSC_OK) rc = maybe_build_mfma(*out, csp, csn, rip, rin, col_begin, st);
         if (rc != TCSC_OK) {
             tcsc_gpu_plan_destroy(*out);
             *out = nullptr;
@@ -416,6 +461,7 @@ int slices_override() {
 // Workspace of one call = [X^T: xt_bytes(M, K)] [split-K slabs, if any].
 size_t wanted_workspace(const tcsc_gpu_plan* p, int M) {
     if (use_mfma(p, M)) return mfma_ws_bytes(M, p->rows);
+    if (use_small(p, M)) return align256((size_t)M * p->rows * sizeof(float));  // staged X (prepare_x)
     const int s = tcsc::choose_slices(M, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
                                       slices_override());
     return tcsc::xt_bytes(M, p->rows) + tcsc::workspace_bytes(M, p->cols, s);
@@ -589,6 +635,24 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
         return TCSC_E_ARG;
     }
     if (use_mfma(p, M)) return sgemm_mfma(p, dX, dB, dY, M, ldy, variant, a, stream, ws, ws_bytes, stage);
+    if (use_small(p, M)) {
+        // stage 1 stages X as is (the kernel reads X rows directly), stage 2 reads the staged copy
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        const size_t xb = (size_t)M * p->rows * sizeof(float);
+        if (stage != 0 && (!ws || ws_bytes < xb)) {
+            set_error("tcsc_gpu_sgemm: workspace of %zu bytes < %zu needed for M=%d", ws ? ws_bytes : (size_t)0, xb,
+                      M);
+            return TCSC_E_ARG;
+        }
+        if (stage == 1) {
+            HIP_TRY(hipMemcpyAsync(ws, dX, xb, hipMemcpyDeviceToDevice, st));
+            return TCSC_OK;
+        }
+        HIP_TRY(tcsc::launch_small_m(stage == 2 ? ws : dX, M, p->rows, p->ccp, p->ccn, p->crp, p->crn, p->cols, dB,
+                                     dY, ldy, variant == TCSC_VARIANT_BASIC, variant >= TCSC_VARIANT_PRELU_BASIC, a,
+                                     st));
+        return TCSC_OK;
+    }
     const size_t xtb = tcsc::xt_bytes(M, p->rows);
     if (p->rows > 0 && (!ws || ws_bytes < xtb)) {
         set_error("tcsc_gpu_sgemm: workspace of %zu bytes < %zu needed for M=%d", ws ? ws_bytes : (size_t)0, xtb, M);
@@ -766,7 +830,7 @@ int tcsc_gpu_plan_get_info(const tcsc_gpu_plan* p, tcsc_gpu_plan_info* info) {
     info->n_neg = p->n_neg;
     info->chunk_k = tcsc::kTK;
     info->n_chunks = p->n_chunks;
-    info->device_bytes = p->bytes + p->ws_bytes + p->mfma_bytes + (p->chain_pos ? p->chain_pos->bytes : 0) +
+    info->device_bytes = p->bytes + p->ws_bytes + p->mfma_bytes + p->csc_bytes + (p->chain_pos ? p->chain_pos->bytes : 0) +
                          (p->chain_neg ? p->chain_neg->bytes : 0);
     info->order = p->order;
     info->mfma_min_M = p->w3 ? p->mfma_min_M : 0;
@@ -787,6 +851,7 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan* p) {
     if (p->sptr) (void)hipFree(p->sptr);
     if (p->ws) (void)hipFree(p->ws);
     free_mfma(p);
+    free_csc(p);
     tcsc_gpu_plan_destroy(p->chain_pos);
     tcsc_gpu_plan_destroy(p->chain_neg);
     delete p;

@@ -156,14 +156,27 @@ hipError_t sort_columns(const int* in, int* out, int n, int ncols, const int* of
 int ldxt_for(int M);
 hipError_t launch_transpose(const float* X, int M, int K, float* XT, int ldxt, hipStream_t st);
 
+// ---- per-column CSC copy of a plan's range (small-M path, MFMA fixup) ------
+// cp/cn (ncols+1) and crp/crn (n_pos/n_neg) <- columns [col_begin,
+// col_begin+ncols) of the absolute-offset arrays, rebased.
+hipError_t csc_copy(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int ncols,
+                    long long n_pos, long long n_neg, int* cp, int* cn, int* crp, int* crn, hipStream_t st);
+
 // ---- MFMA path for near-dense W (tcsc_mfma.hip) ------------
 // Build: wf (ncols x rows fp32 scratch) <- the +1/-1 entries of columns
 // [col_begin, col_begin+ncols) (absolute offsets), transposed; w3 <- W^T
-// with three bf16 copies per row (ncols x 3*rows); cp/cn (ncols+1) and crp/crn (n_pos/n_neg) <- the range's
-// rebased CSC copy.  *bad = 1 if a weight is not exact in bf16.
+// with three bf16 copies per row (ncols x 3*rows).  *bad = 1 if a weight is
+// not exact in bf16.
 hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int rows,
-                         int ncols, float* wf, uint16_t* w3, int* cp, int* cn, int* crp, int* crn, long long n_pos,
-                         long long n_neg, int* bad, hipStream_t st);
+                         int ncols, float* wf, uint16_t* w3, long long n_pos, long long n_neg, int* bad,
+                         hipStream_t st);
+
+// ---- small-M path (tcsc_small.hip) ----------------------------
+// Y[m, j] = act(B[j] + sum_P X[m,k] - sum_Q X[m,k]) for m < M <= 16, one wave
+// per column over the CSC copy.
+hipError_t launch_small_m(const float* X, int M, int K, const int* cp, const int* cn, const int* crp, const int* crn,
+                          int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
+                          hipStream_t st);
 // X (M x K) -> x3 (M x 3K bf16, [h | m | l]); flags[M] + *any (= flags + M)
 // mark the rows the fixup recomputes.
 hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int* flags, int* any, hipStream_t st);

@@ -181,9 +181,21 @@ __global__ void k_fixup(const uint16_t* __restrict__ X3, int M, int K, const int
 
 }  // namespace
 
+hipError_t csc_copy(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int ncols,
+                    long long n_pos, long long n_neg, int* cp, int* cn, int* crp, int* crn, hipStream_t st) {
+    hipError_t e;
+    if ((e = rebase_offsets(csp, col_begin, ncols, cp, st)) != hipSuccess) return e;
+    if ((e = rebase_offsets(csn, col_begin, ncols, cn, st)) != hipSuccess) return e;
+    if (n_pos > 0)
+        hipLaunchKernelGGL(k_copy_from, dim3(grid_of(n_pos, 256)), dim3(256), 0, st, rip, csp, col_begin, n_pos, crp);
+    if (n_neg > 0)
+        hipLaunchKernelGGL(k_copy_from, dim3(grid_of(n_neg, 256)), dim3(256), 0, st, rin, csn, col_begin, n_neg, crn);
+    return hipGetLastError();
+}
+
 hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int rows,
-                         int ncols, float* wf, uint16_t* w3, int* cp, int* cn, int* crp, int* crn, long long n_pos,
-                         long long n_neg, int* bad, hipStream_t st) {
+                         int ncols, float* wf, uint16_t* w3, long long n_pos, long long n_neg, int* bad,
+                         hipStream_t st) {
     const long long n = (long long)rows * ncols;
     hipError_t e = hipMemsetAsync(wf, 0, (size_t)n * sizeof(float), st);
     if (e != hipSuccess) return e;
@@ -195,12 +207,6 @@ hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const i
         hipLaunchKernelGGL(k_w_scatter, dim3((ncols + wpb - 1) / wpb), dim3(64 * wpb), 0, st, csn, rin, col_begin,
                            ncols, rows, -1.0f, wf);
     hipLaunchKernelGGL(k_w3_from, dim3(grid_of(n, 256)), dim3(256), 0, st, wf, ncols, rows, w3, bad);
-    if ((e = rebase_offsets(csp, col_begin, ncols, cp, st)) != hipSuccess) return e;
-    if ((e = rebase_offsets(csn, col_begin, ncols, cn, st)) != hipSuccess) return e;
-    if (n_pos > 0)
-        hipLaunchKernelGGL(k_copy_from, dim3(grid_of(n_pos, 256)), dim3(256), 0, st, rip, csp, col_begin, n_pos, crp);
-    if (n_neg > 0)
-        hipLaunchKernelGGL(k_copy_from, dim3(grid_of(n_neg, 256)), dim3(256), 0, st, rin, csn, col_begin, n_neg, crn);
     return hipGetLastError();
 }
 
