@@ -68,6 +68,7 @@ struct tcsc_gpu_plan {
     // take it; null when the plan is gather-only.
     uint16_t* w3 = nullptr;
     size_t mfma_bytes = 0;
+    int mfma_gen = 0;  // staging generation of the MFMA path's row flags
     // the column range's rebased CSC (fast-order plans): the small-M path
     // walks it, the MFMA path's fixup recomputes flagged rows from it
     int *ccp = nullptr, *ccn = nullptr, *crp = nullptr, *crn = nullptr;
@@ -581,7 +582,11 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
     uint16_t* x3 = reinterpret_cast<uint16_t*>(ws);
     int* flags = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + align256((size_t)M * 3 * K * 2));
     int* any = flags + M;
-    if (stage != 2) HIP_TRY(tcsc::mfma_split_x(dX, M, K, x3, flags, any, st));
+    tcsc_gpu_plan* mp = const_cast<tcsc_gpu_plan*>(p);
+    if (stage != 2) {
+        mp->mfma_gen = mp->mfma_gen == 0x7fffffff ? 1 : mp->mfma_gen + 1;
+        HIP_TRY(tcsc::mfma_split_x(dX, M, K, x3, flags, any, mp->mfma_gen, st));
+    }
     if (stage == 1) return TCSC_OK;
     const float one = 1.0f, zero = 0.0f;
     const bool prelu = variant >= TCSC_VARIANT_PRELU_BASIC;
@@ -619,7 +624,7 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
     }
     if (!bias_done) HIP_TRY(tcsc::launch_bias_act(dY, M, N, ldy, dB, prelu, a, st));
     HIP_TRY(tcsc::mfma_fixup(x3, M, K, p->ccp, p->ccn, p->crp, p->crn, N, dB, dY, ldy,
-                             variant == TCSC_VARIANT_BASIC, prelu, a, flags, any, st));
+                             variant == TCSC_VARIANT_BASIC, prelu, a, flags, any, mp->mfma_gen, st));
     return TCSC_OK;
 }
 

@@ -177,13 +177,13 @@ hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const i
 hipError_t launch_small_m(const float* X, int M, int K, const int* cp, const int* cn, const int* crp, const int* crn,
                           int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
                           hipStream_t st);
-// X (M x K) -> x3 (M x 3K bf16, [h | m | l]); flags[M] + *any (= flags + M)
-// mark the rows the fixup recomputes.
-hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int* flags, int* any, hipStream_t st);
-// Rewrites the flagged rows of Y in k_stream's fast order (no-op if *any == 0).
+// X (M x K) -> x3 (M x 3K bf16, [h | m | l]); flags[m] = gen and *any (=
+// flags + M) = gen mark the rows the fixup recomputes (gen: new per staging).
+hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int* flags, int* any, int gen, hipStream_t st);
+// Rewrites the rows flagged with gen in k_stream's fast order (no-op if *any != gen).
 hipError_t mfma_fixup(const uint16_t* x3, int M, int K, const int* cp, const int* cn, const int* crp, const int* crn,
                       int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
-                      const int* flags, const int* any, hipStream_t st);
+                      const int* flags, const int* any, int gen, hipStream_t st);
 
 // Error channel shared by every entry point of the library (tcsc_api.cpp):
 // the message behind tcsc_gpu_last_error(), and the host API's policy

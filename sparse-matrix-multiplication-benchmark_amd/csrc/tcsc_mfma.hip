@@ -62,9 +62,11 @@ __device__ inline bool split3(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
 }
 
 // X (M x K, pitch K) -> X3 (M x 3K bf16, pitch 3K): [h | m | l] per row.
-// flags[m] = 1 (and *any = 1) for a row the fixup must recompute.
+// flags[m] = gen (and *any = gen) for a row the fixup must recompute; gen
+// is new for every staging, so the flags need no clearing (a stale value
+// equal to gen could only make the fixup recompute a row exactly).
 __global__ void k_split3(const float* __restrict__ X, int M, int K, uint16_t* __restrict__ X3,
-                         int* __restrict__ flags, int* __restrict__ any) {
+                         int* __restrict__ flags, int* __restrict__ any, int gen) {
     const int kq = (K + 3) / 4;
     const long long total = (long long)M * kq;
     const bool vec = (K & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
@@ -97,8 +99,8 @@ __global__ void k_split3(const float* __restrict__ X, int M, int K, uint16_t* __
             }
         }
         if (fix) {
-            flags[row] = 1;
-            *any = 1;
+            flags[row] = gen;
+            *any = gen;
         }
     }
 }
@@ -151,13 +153,13 @@ template <bool BIAS_FIRST, bool PRELU>
 __global__ void k_fixup(const uint16_t* __restrict__ X3, int M, int K, const int* __restrict__ cp,
                         const int* __restrict__ cn, const int* __restrict__ rp, const int* __restrict__ rn,
                         int ncols, const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a,
-                        const int* __restrict__ flags, const int* __restrict__ any) {
-    if (*any == 0) return;
+                        const int* __restrict__ flags, const int* __restrict__ any, int gen) {
+    if (*any != gen) return;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= ncols) return;
     const int p1 = cp[j + 1], q1 = cn[j + 1];
     for (int row = 0; row < M; ++row) {
-        if (flags[row] == 0) continue;
+        if (flags[row] != gen) continue;
         const uint16_t* x3 = X3 + (size_t)row * 3 * K;
         auto xk = [&](int k) {
             return (u2f((uint32_t)x3[k] << 16) + u2f((uint32_t)x3[K + k] << 16)) + u2f((uint32_t)x3[2 * K + k] << 16);
@@ -210,32 +212,30 @@ hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const i
     return hipGetLastError();
 }
 
-hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int* flags, int* any, hipStream_t st) {
-    hipError_t e = hipMemsetAsync(flags, 0, (size_t)(M + 1) * sizeof(int), st);  // flags[0..M-1], then *any
-    if (e != hipSuccess) return e;
+hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int* flags, int* any, int gen, hipStream_t st) {
     const long long total = (long long)M * ((K + 3) / 4);
-    hipLaunchKernelGGL(k_split3, dim3(grid_of(total, 256)), dim3(256), 0, st, X, M, K, x3, flags, any);
+    hipLaunchKernelGGL(k_split3, dim3(grid_of(total, 256)), dim3(256), 0, st, X, M, K, x3, flags, any, gen);
     return hipGetLastError();
 }
 
 hipError_t mfma_fixup(const uint16_t* x3, int M, int K, const int* cp, const int* cn, const int* crp, const int* crn,
                       int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
-                      const int* flags, const int* any, hipStream_t st) {
+                      const int* flags, const int* any, int gen, hipStream_t st) {
     const dim3 grid((ncols + 255) / 256), block(256);
     if (bias_first) {
         if (prelu)
             hipLaunchKernelGGL((k_fixup<true, true>), grid, block, 0, st, x3, M, K, cp, cn, crp, crn, ncols, B, Y, ldy,
-                               a, flags, any);
+                               a, flags, any, gen);
         else
             hipLaunchKernelGGL((k_fixup<true, false>), grid, block, 0, st, x3, M, K, cp, cn, crp, crn, ncols, B, Y,
-                               ldy, a, flags, any);
+                               ldy, a, flags, any, gen);
     } else {
         if (prelu)
             hipLaunchKernelGGL((k_fixup<false, true>), grid, block, 0, st, x3, M, K, cp, cn, crp, crn, ncols, B, Y,
-                               ldy, a, flags, any);
+                               ldy, a, flags, any, gen);
         else
             hipLaunchKernelGGL((k_fixup<false, false>), grid, block, 0, st, x3, M, K, cp, cn, crp, crn, ncols, B, Y,
-                               ldy, a, flags, any);
+                               ldy, a, flags, any, gen);
     }
     return hipGetLastError();
 }
