@@ -622,9 +622,14 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
             return TCSC_E_HIP;
         }
     }
-    if (!bias_done) HIP_TRY(tcsc::launch_bias_act(dY, M, N, ldy, dB, prelu, a, st));
-    HIP_TRY(tcsc::mfma_fixup(x3, M, K, p->ccp, p->ccn, p->crp, p->crn, N, dB, dY, ldy,
-                             variant == TCSC_VARIANT_BASIC, prelu, a, flags, any, mp->mfma_gen, st));
+    // bias (+ PReLU) and the flagged rows' exact values in one pass, or only
+    // the flagged rows when the GEMM's epilogue added the bias
+    if (!bias_done)
+        HIP_TRY(tcsc::mfma_epilogue_fix(x3, M, K, p->ccp, p->ccn, p->crp, p->crn, N, dB, dY, ldy,
+                                        variant == TCSC_VARIANT_BASIC, prelu, a, flags, any, mp->mfma_gen, st));
+    else
+        HIP_TRY(tcsc::mfma_fixup(x3, M, K, p->ccp, p->ccn, p->crp, p->crn, N, dB, dY, ldy,
+                                 variant == TCSC_VARIANT_BASIC, prelu, a, flags, any, mp->mfma_gen, st));
     return TCSC_OK;
 }
 

@@ -180,6 +180,11 @@ hipError_t launch_small_m(const float* X, int M, int K, const int* cp, const int
 // X (M x K) -> x3 (M x 3K bf16, [h | m | l]); flags[m] = gen and *any (=
 // flags + M) = gen mark the rows the fixup recomputes (gen: new per staging).
 hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int* flags, int* any, int gen, hipStream_t st);
+// Y = act(Y + B) with the rows flagged with gen recomputed exactly (the
+// epilogue after a GEMM without the bias).
+hipError_t mfma_epilogue_fix(const uint16_t* x3, int M, int K, const int* cp, const int* cn, const int* crp,
+                             const int* crn, int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu,
+                             float a, const int* flags, const int* any, int gen, hipStream_t st);
 // Rewrites the rows flagged with gen in k_stream's fast order (no-op if *any != gen).
 hipError_t mfma_fixup(const uint16_t* x3, int M, int K, const int* cp, const int* cn, const int* crp, const int* crn,
                       int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,

@@ -147,8 +147,37 @@ __global__ void k_copy_from(const int* __restrict__ src, const int* __restrict__
         dst[i] = src[base + i];
 }
 
-// Flagged rows, recomputed exactly as k_stream's fast order (see the file
-// comment).  One thread per column; every block walks the flag list.
+// Output (row, j) recomputed exactly as k_stream's fast order (see the file
+// comment): x rebuilt from its three parts, +1 and -1 rows merged in
+// ascending k, the bias first or last, then the PReLU.
+template <bool BIAS_FIRST, bool PRELU>
+__device__ inline float exact_out(const uint16_t* __restrict__ X3, int K, const int* __restrict__ cp,
+                                  const int* __restrict__ cn, const int* __restrict__ rp,
+                                  const int* __restrict__ rn, const float* __restrict__ Bias, int row, int j,
+                                  float a) {
+    const uint16_t* x3 = X3 + (size_t)row * 3 * K;
+    auto xk = [&](int k) {
+        return (u2f((uint32_t)x3[k] << 16) + u2f((uint32_t)x3[K + k] << 16)) + u2f((uint32_t)x3[2 * K + k] << 16);
+    };
+    float acc = BIAS_FIRST ? Bias[j] : 0.0f;
+    int p = cp[j], q = cn[j];
+    const int p1 = cp[j + 1], q1 = cn[j + 1];
+    while (p < p1 || q < q1) {
+        if (q >= q1 || (p < p1 && rp[p] <= rn[q])) {
+            acc = fmaf(xk(rp[p]), 1.0f, acc);
+            ++p;
+        } else {
+            acc = fmaf(xk(rn[q]), -1.0f, acc);
+            ++q;
+        }
+    }
+    if (!BIAS_FIRST) acc += Bias[j];
+    if (PRELU) acc = (acc < 0.0f) ? a * acc : acc;
+    return acc;
+}
+
+// Flagged rows, after a GEMM that already added the bias (no PReLU).  One
+// thread per column; every block walks the flag list.
 template <bool BIAS_FIRST, bool PRELU>
 __global__ void k_fixup(const uint16_t* __restrict__ X3, int M, int K, const int* __restrict__ cp,
                         const int* __restrict__ cn, const int* __restrict__ rp, const int* __restrict__ rn,
@@ -157,27 +186,52 @@ __global__ void k_fixup(const uint16_t* __restrict__ X3, int M, int K, const int
     if (*any != gen) return;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= ncols) return;
-    const int p1 = cp[j + 1], q1 = cn[j + 1];
-    for (int row = 0; row < M; ++row) {
-        if (flags[row] != gen) continue;
-        const uint16_t* x3 = X3 + (size_t)row * 3 * K;
-        auto xk = [&](int k) {
-            return (u2f((uint32_t)x3[k] << 16) + u2f((uint32_t)x3[K + k] << 16)) + u2f((uint32_t)x3[2 * K + k] << 16);
-        };
-        float acc = BIAS_FIRST ? Bias[j] : 0.0f;
-        int p = cp[j], q = cn[j];
-        while (p < p1 || q < q1) {
-            if (q >= q1 || (p < p1 && rp[p] <= rn[q])) {
-                acc = fmaf(xk(rp[p]), 1.0f, acc);
-                ++p;
-            } else {
-                acc = fmaf(xk(rn[q]), -1.0f, acc);
-                ++q;
+    for (int row = 0; row < M; ++row)
+        if (flags[row] == gen)
+            Y[(size_t)row * ldy + j] = exact_out<BIAS_FIRST, PRELU>(X3, K, cp, cn, rp, rn, Bias, row, j, a);
+}
+
+// The epilogue after a plain GEMM, with the fixup folded in: Y = act(Y + B)
+// for the rows the split carried, the exact fast-order value for the
+// flagged ones.  One launch instead of two.
+template <bool BIAS_FIRST, bool PRELU>
+__global__ void k_epilogue_fix(float* __restrict__ Y, int M, int N, int ldy, const float* __restrict__ Bias, float a,
+                               const uint16_t* __restrict__ X3, int K, const int* __restrict__ cp,
+                               const int* __restrict__ cn, const int* __restrict__ rp, const int* __restrict__ rn,
+                               const int* __restrict__ flags, const int* __restrict__ any, int gen) {
+    const bool some = *any == gen;
+    const int nq = (N + 3) / 4;
+    const long long total = (long long)M * nq;
+    const bool vec = (ldy & 3) == 0 && (N & 3) == 0 && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0);
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int m = (int)(i / nq), n = 4 * (int)(i % nq);
+        float* y = Y + (size_t)m * ldy + n;
+        if (some && flags[m] == gen) {
+            for (int c = 0; c < 4 && n + c < N; ++c)
+                y[c] = exact_out<BIAS_FIRST, PRELU>(X3, K, cp, cn, rp, rn, Bias, m, n + c, a);
+            continue;
+        }
+        if (vec) {
+            float4 v = *reinterpret_cast<float4*>(y);
+            v.x += Bias[n + 0];
+            v.y += Bias[n + 1];
+            v.z += Bias[n + 2];
+            v.w += Bias[n + 3];
+            if (PRELU) {
+                v.x = (v.x < 0.0f) ? a * v.x : v.x;
+                v.y = (v.y < 0.0f) ? a * v.y : v.y;
+                v.z = (v.z < 0.0f) ? a * v.z : v.z;
+                v.w = (v.w < 0.0f) ? a * v.w : v.w;
+            }
+            *reinterpret_cast<float4*>(y) = v;
+        } else {
+            for (int c = 0; c < 4 && n + c < N; ++c) {
+                float v = y[c] + Bias[n + c];
+                if (PRELU) v = (v < 0.0f) ? a * v : v;
+                y[c] = v;
             }
         }
-        if (!BIAS_FIRST) acc += Bias[j];
-        if (PRELU) acc = (acc < 0.0f) ? a * acc : acc;
-        Y[(size_t)row * ldy + j] = acc;
     }
 }
 
@@ -215,6 +269,27 @@ hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const i
 hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int* flags, int* any, int gen, hipStream_t st) {
     const long long total = (long long)M * ((K + 3) / 4);
     hipLaunchKernelGGL(k_split3, dim3(grid_of(total, 256)), dim3(256), 0, st, X, M, K, x3, flags, any, gen);
+    return hipGetLastError();
+}
+
+hipError_t mfma_epilogue_fix(const uint16_t* x3, int M, int K, const int* cp, const int* cn, const int* crp,
+                             const int* crn, int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu,
+                             float a, const int* flags, const int* any, int gen, hipStream_t st) {
+    const long long total = (long long)M * ((ncols + 3) / 4);
+    const dim3 grid(grid_of(total, 256)), block(256);
+#define TCSC_EPI_ARGS Y, M, ncols, ldy, B, a, x3, K, cp, cn, crp, crn, flags, any, gen
+    if (bias_first) {
+        if (prelu)
+            hipLaunchKernelGGL((k_epilogue_fix<true, true>), grid, block, 0, st, TCSC_EPI_ARGS);
+        else
+            hipLaunchKernelGGL((k_epilogue_fix<true, false>), grid, block, 0, st, TCSC_EPI_ARGS);
+    } else {
+        if (prelu)
+            hipLaunchKernelGGL((k_epilogue_fix<false, true>), grid, block, 0, st, TCSC_EPI_ARGS);
+        else
+            hipLaunchKernelGGL((k_epilogue_fix<false, false>), grid, block, 0, st, TCSC_EPI_ARGS);
+    }
+#undef TCSC_EPI_ARGS
     return hipGetLastError();
 }
 
