@@ -634,7 +634,7 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
 }
 
 int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy, int variant,
-             float a, void* stream, float* ws, size_t ws_bytes, int stage = 0) {
+             float a, void* stream, float* ws, size_t ws_bytes, int stage = 0, int force_slices = 0) {
     if (!p || M < 0 || (stage != 1 && (ldy < p->cols || variant < 0 || variant > 4))) {
         set_error("tcsc_gpu_sgemm: bad arguments (M=%d ldy=%d variant=%d)", M, ldy, variant);
         return TCSC_E_ARG;
@@ -696,7 +696,7 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
     g.a = a;
     g.ws = (ws && ws_bytes > xtb) ? reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + xtb) : nullptr;
     g.ws_bytes = g.ws ? ws_bytes - xtb : 0;
-    g.force_slices = slices_override();
+    g.force_slices = force_slices > 0 ? force_slices : slices_override();
     g.stage = stage;
     // Bias first for tcsc_sgemm_basic (tcsc.c:74-96), last otherwise
     // (tcsc.c:149-161; the optimized family adds per-sign partial sums to
@@ -1047,11 +1047,13 @@ struct CacheEntry {
     std::vector<Shard> shards;    // cols: one per column block; rows: one per device used
 };
 
-// Per-device staging buffers for X, B and Y of the host API.
+// Per-device staging buffers for X, B and Y of the host API, and the copy
+// streams and events of the banded pipeline (run_device).
 struct DevState {
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr, s_in = nullptr, s_out = nullptr;
     float *x = nullptr, *b = nullptr, *y = nullptr, *ws = nullptr;
     size_t x_cap = 0, b_cap = 0, y_cap = 0, ws_cap = 0;
+    std::vector<hipEvent_t> ev_in, ev_k;
 };
 
 std::mutex g_mu;  // guards everything below (host API is re-entrant, not concurrent-fast)
@@ -1169,9 +1171,37 @@ struct Job {
     int m0, m1;
 };
 
+// Row bands of one job for the copy/compute pipeline: X arrives from pageable
+// host memory at ~50 GB/s, so at cfg 4 the H2D of X and the D2H of Y take
+// ~10 ms against 1.3 ms of kernels.  Split into bands (whole 256-row tiles,
+// >= 32 MB of X each, at most 8), band b's kernels run while band b+1's X
+// and band b-1's Y cross PCIe.  Only on the gather path with the split-K
+// factor of the whole job forced on every band: each element is then summed
+// in the same order as by one launch, so the bits do not change.
+// TCSC_HOST_BANDS=1 turns the pipeline off, =n asks for n bands.
+int host_bands(const tcsc_gpu_plan* p, int M, int K) {
+    if (use_mfma(p, M) || use_small(p, M) || K <= 0) return 1;
+    const double xbytes = (double)M * K * sizeof(float);
+    int nb = (int)(xbytes / (32.0 * 1024 * 1024));
+    if (const char* e = std::getenv("TCSC_HOST_BANDS")) nb = std::atoi(e);
+    nb = std::min(nb, 8);
+    nb = std::min(nb, M / tcsc::kTM);  // whole row tiles
+    return nb < 2 ? 1 : nb;
+}
+
+int ensure_events(std::vector<hipEvent_t>& v, size_t n) {
+    while (v.size() < n) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        v.push_back(e);
+    }
+    return TCSC_OK;
+}
+
 // Everything one device does for one call, job by job: H2D of the job's rows
 // of X (skipped when the previous job staged the same rows), H2D of the bias
-// slice, the launch, D2H of the (m1-m0) x (c1-c0) block into Y.
+// slice, the launch, D2H of the (m1-m0) x (c1-c0) block into Y.  A large job
+// runs as a pipeline of row bands over three streams (host_bands).
 int run_device(int dev, const std::vector<Job>& jobs, const float* X, const float* B, float* Y, int N, int K,
                int variant, float a) {
     DeviceGuard dg(dev);
@@ -1182,6 +1212,52 @@ int run_device(int dev, const std::vector<Job>& jobs, const float* X, const floa
         const Shard* sh = j.sh;
         const int nc = sh->c1 - sh->c0, M = j.m1 - j.m0;
         if (nc == 0 || M == 0) continue;
+        const int nb = (j.m0 != staged0 || j.m1 != staged1) ? host_bands(sh->plan, M, K) : 1;
+        if ((rc = ensure(&ds.b, &ds.b_cap, (size_t)nc * sizeof(float))) != TCSC_OK) return rc;
+        if ((rc = ensure(&ds.y, &ds.y_cap, (size_t)M * nc * sizeof(float))) != TCSC_OK) return rc;
+        if (nb > 1) {
+            const tcsc_gpu_plan* p = sh->plan;
+            const int s = tcsc::choose_slices(M, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
+                                              slices_override());
+            const int rows_per = (M + nb - 1) / nb;
+            const int bm = (rows_per + tcsc::kTM - 1) / tcsc::kTM * tcsc::kTM;
+            const size_t wsb = tcsc::xt_bytes(bm, K) + tcsc::workspace_bytes(bm, nc, s);
+            if ((rc = ensure(&ds.x, &ds.x_cap, (size_t)M * K * sizeof(float))) != TCSC_OK) return rc;
+            if ((rc = ensure(&ds.ws, &ds.ws_cap, wsb)) != TCSC_OK) return rc;
+            if (!ds.s_in) HIP_TRY(hipStreamCreateWithFlags(&ds.s_in, hipStreamNonBlocking));
+            if (!ds.s_out) HIP_TRY(hipStreamCreateWithFlags(&ds.s_out, hipStreamNonBlocking));
+            if ((rc = ensure_events(ds.ev_in, nb)) != TCSC_OK || (rc = ensure_events(ds.ev_k, nb)) != TCSC_OK)
+                return rc;
+            HIP_TRY(hipMemcpyAsync(ds.b, B + sh->c0, (size_t)nc * sizeof(float), hipMemcpyHostToDevice, st));
+            auto d2h = [&](int b) -> int {
+                const int r0 = b * bm, r1 = std::min(M, r0 + bm);
+                HIP_TRY(hipStreamWaitEvent(ds.s_out, ds.ev_k[b], 0));
+                HIP_TRY(hipMemcpy2DAsync(Y + (size_t)(j.m0 + r0) * N + sh->c0, (size_t)N * sizeof(float),
+                                         ds.y + (size_t)r0 * nc, (size_t)nc * sizeof(float),
+                                         (size_t)nc * sizeof(float), r1 - r0, hipMemcpyDeviceToHost, ds.s_out));
+                return TCSC_OK;
+            };
+            int nbands = 0;
+            for (int b = 0; b * bm < M; ++b, ++nbands) {
+                const int r0 = b * bm, r1 = std::min(M, r0 + bm);
+                float* xb = ds.x + (size_t)r0 * K;
+                HIP_TRY(hipMemcpyAsync(xb, X + (size_t)(j.m0 + r0) * K, (size_t)(r1 - r0) * K * sizeof(float),
+                                       hipMemcpyHostToDevice, ds.s_in));
+                HIP_TRY(hipEventRecord(ds.ev_in[b], ds.s_in));
+                HIP_TRY(hipStreamWaitEvent(st, ds.ev_in[b], 0));
+                if ((rc = sgemm_ws(p, xb, ds.b, ds.y + (size_t)r0 * nc, r1 - r0, nc, variant, a, st, ds.ws,
+                                   ds.ws_cap, 0, s)) != TCSC_OK)
+                    return rc;
+                HIP_TRY(hipEventRecord(ds.ev_k[b], st));
+                if (b > 0 && (rc = d2h(b - 1)) != TCSC_OK) return rc;
+            }
+            if ((rc = d2h(nbands - 1)) != TCSC_OK) return rc;
+            HIP_TRY(hipStreamSynchronize(ds.s_out));
+            HIP_TRY(hipStreamSynchronize(st));
+            staged0 = j.m0;
+            staged1 = j.m1;
+            continue;
+        }
         if (j.m0 != staged0 || j.m1 != staged1) {
             const size_t xb = (size_t)M * K * sizeof(float);
             if ((rc = ensure(&ds.x, &ds.x_cap, xb)) != TCSC_OK) return rc;
@@ -1189,8 +1265,6 @@ int run_device(int dev, const std::vector<Job>& jobs, const float* X, const floa
             staged0 = j.m0;
             staged1 = j.m1;
         }
-        if ((rc = ensure(&ds.b, &ds.b_cap, (size_t)nc * sizeof(float))) != TCSC_OK) return rc;
-        if ((rc = ensure(&ds.y, &ds.y_cap, (size_t)M * nc * sizeof(float))) != TCSC_OK) return rc;
         const size_t wsb = wanted_workspace(sh->plan, M);
         if (wsb && (rc = ensure(&ds.ws, &ds.ws_cap, wsb)) != TCSC_OK) return rc;
         HIP_TRY(hipMemcpyAsync(ds.b, B + sh->c0, (size_t)nc * sizeof(float), hipMemcpyHostToDevice, st));

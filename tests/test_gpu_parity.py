@@ -202,6 +202,34 @@ def test_multi_shard_host_path_large(gpu, oracle, axis, monkeypatch):
     W.free()
 
 
+@pytest.mark.parametrize("M,K,N,bands", [(1024, 1500, 700, 4), (1100, 700, 300, 3), (2000, 2600, 96, 8)])
+def test_host_bands_bit_identical(gpu, torch_cuda, oracle, M, K, N, bands, monkeypatch):
+    """The host API's copy/compute pipeline (row bands over three streams,
+    TCSC_HOST_BANDS) gives the bits of one device launch, split-K included
+    (N=96: few column blocks, so K is split), ragged last band included."""
+    torch = torch_cuda
+    Wd = oracle.ternary((K, N), 0.05, 700 + M)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    X, B = oracle.uniform((M, K), 701 + M), oracle.uniform((N,), 702 + M)
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.current_stream().cuda_stream
+    plan = tcsc_amd.Plan(W, 0, N, 0, stream)
+    plan.reserve(M)
+    dX, dB = torch.from_numpy(X).to(dev), torch.from_numpy(B).to(dev)
+    monkeypatch.setenv("TCSC_HOST_BANDS", str(bands))
+    for variant in pyoracle.VARIANTS:
+        Yd = torch.empty((M, N), device=dev)
+        plan.sgemm(dX, dB, Yd, M, N, variant, 0.2, stream)
+        torch.cuda.synchronize()
+        Yh = tcsc_amd.sgemm(variant, X, W, B, 0.2)
+        np.testing.assert_array_equal(Yh.view(np.uint32), Yd.cpu().numpy().view(np.uint32), err_msg=variant)
+        monkeypatch.setenv("TCSC_HOST_BANDS", "1")  # the unbanded host path, same bits
+        np.testing.assert_array_equal(tcsc_amd.sgemm(variant, X, W, B, 0.2).view(np.uint32), Yh.view(np.uint32))
+        monkeypatch.setenv("TCSC_HOST_BANDS", str(bands))
+    plan.destroy()
+    W.free()
+
+
 def test_device_plan_from_device_arrays_and_gpu_builder(gpu, torch_cuda, oracle):
     torch = torch_cuda
     dev = torch.device("cuda:0")
