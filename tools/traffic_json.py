@@ -3,8 +3,11 @@
 
 FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE
 counts half the bytes of 16-B-per-lane streaming reads (the LDS-DMA of X^T
-is exactly that), so it is doubled (MI355X_MICROARCH.md "HBM"); WRITE_SIZE
-is exact for the kernel's 16-B row stores.  Writes profiles/traffic.json
+is exactly that), so that part is doubled (MI355X_MICROARCH.md "HBM");
+WRITE_SIZE is exact for the kernel's 16-B row stores.  The other fetches are
+the entry streams' scalar loads: pass 4 measures them alone (the no-DMA
+ablation build), and they are taken as counted (16 row tiles x the 49 MB
+plan is 783 MB, what the pass reads).  Writes profiles/traffic.json
 keyed like bench.py looks it up ("cfg4:prelu_basic:16384").  Run it where
 gpurun_out/ holds the passes (here, after gpurun merged them back)."""
 import collections
@@ -35,6 +38,7 @@ def main():
     out = os.path.join(ROOT, "gpurun_out")
     fetch = per_dispatch(os.path.join(out, "traffic1"), "FETCH_SIZE")
     write = per_dispatch(os.path.join(out, "traffic2"), "WRITE_SIZE")
+    nodma = per_dispatch(os.path.join(out, "traffic4"), "FETCH_SIZE")
     hit = per_dispatch(os.path.join(out, "traffic3"), "TCC_HIT_sum")
     miss = per_dispatch(os.path.join(out, "traffic3"), "TCC_MISS_sum")
     if not fetch or not write:
@@ -42,14 +46,21 @@ def main():
         return 1
     f_kib = sum(fetch) / len(fetch)
     w_kib = sum(write) / len(write)
+    s_kib = sum(nodma) / len(nodma) if nodma else 0.0  # entry streams (scalar loads)
+    x_kib = f_kib - s_kib                               # X^T through the LDS-DMA (16 B/lane)
     rec = {
         "kernel": KERNEL,
         "fetch_size_kib_raw": f_kib,
+        "stream_fetch_kib_raw": s_kib if nodma else None,
         "write_size_kib": w_kib,
-        "hbm_bytes_per_launch": (2.0 * f_kib + w_kib) * 1024.0,
-        "correction": "FETCH_SIZE x2 (gfx950, 16-B/lane streaming reads), WRITE_SIZE as is",
+        "xt_bytes": 2.0 * x_kib * 1024.0,
+        "stream_bytes": s_kib * 1024.0,
+        "write_bytes": w_kib * 1024.0,
+        "hbm_bytes_per_launch": (2.0 * x_kib + s_kib + w_kib) * 1024.0,
+        "correction": "FETCH_SIZE x2 for the X^T part (gfx950, 16-B/lane streaming reads), the entry-stream "
+                      "part (no-DMA ablation pass) and WRITE_SIZE as counted",
         "l2_hit_rate": (sum(hit) / (sum(hit) + sum(miss))) if hit and miss else None,
-        "dispatches": [len(fetch), len(write)],
+        "dispatches": [len(fetch), len(write), len(nodma)],
     }
     path = os.path.join(ROOT, "profiles", "traffic.json")
     data = {}
