@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--no-other-configs", action="store_true",
                    help="skip the other BASELINE configs' timings (N=1 only)")
     p.add_argument("--no-validate", action="store_true", help="skip the pre-timing check against the dense product")
+    p.add_argument("--no-host-api", action="store_true",
+                   help="skip the drop-in host-pointer call line (PCIe included; N=1 only)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
     p.add_argument("--override", default="", help="experiments only: e.g. 'K=16448,N=4096' (marks the line)")
     return p.parse_args()
@@ -288,6 +290,12 @@ def main():
             del Yd
         if Wd is not None and not args.no_bcsr:
             out["bcsr"] = bcsr_line(cfg, Wd, X, B, Y, nnz, gather_s, timed, sh, nsplit)
+        if world == 1 and not args.no_host_api:
+            # end to end through the drop-in symbol, H2D of X/B and D2H of Y
+            # included (pageable numpy buffers, as main.cpp passes them); Y still holds the
+            # device API's output of the same X, so the two are compared bit for bit
+            out["host_api"] = host_api_line(tcsc_amd, cfg, ncols, variant, X, B, Y, csp, csn, rip[:npos],
+                                            rin[:nneg], adds_per_launch)
         if world == 1 and not args.no_reference_order:
             # include/tcsc_gpu.h TCSC_ORDER_REFERENCE: each variant in the reference's own
             # summation order (float outputs bit-identical to sparse/tcsc.c); K is walked once
@@ -314,6 +322,35 @@ def main():
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def host_api_line(tcsc_amd, cfg, ncols, variant, X, B, Y, csp, csn, rip, rin, adds, calls=3):
+    """tcsc_sgemm_<variant> (sparse/tcsc.h:21-46) on host copies of the same
+    inputs: the first call (plan build + W upload) and the mean of `calls`
+    steady-state calls, each synchronous with its PCIe copies (not `value`)."""
+    import numpy as np
+
+    Xh, Bh, Yd = X.cpu().numpy(), B.cpu().numpy(), Y.cpu().numpy()
+    W = tcsc_amd.TcscMatrix.from_arrays(cfg.K, ncols, csp.cpu().numpy(), csn.cpu().numpy(), rip.cpu().numpy(),
+                                        rin.cpu().numpy())
+    Yh = np.zeros((cfg.M, ncols), np.float32)
+    t0 = time.perf_counter()
+    tcsc_amd.sgemm(variant, Xh, W, Bh, 0.2, Yh)
+    first = time.perf_counter() - t0
+    same = bool(np.array_equal(Yh.view(np.uint32), Yd.view(np.uint32)))
+    ts = []
+    for _ in range(calls):
+        t0 = time.perf_counter()
+        tcsc_amd.sgemm(variant, Xh, W, Bh, 0.2, Yh)
+        ts.append(time.perf_counter() - t0)
+    tcsc_amd.cache_clear()
+    W.free()
+    ms = sum(ts) / len(ts) * 1e3
+    return {"symbol": f"tcsc_sgemm_{variant}", "ms": ms, "g_add_ops_per_s": adds / (ms * 1e-3) / 1e9,
+            "first_call_ms": first * 1e3, "calls": calls,
+            "pcie_bytes": 4 * (cfg.M * cfg.K + cfg.M * ncols + ncols),
+            "bit_identical_to_device_api": same,
+            "note": "pageable host X/B/Y; H2D + kernels + D2H, row bands pipelined over 3 streams"}
 
 
 def other_configs(tcsc_amd, workloads, dev, sh, timed, skip):
