@@ -32,7 +32,12 @@ enum tcsc_variant {
     TCSC_VARIANT_OPTIMIZED = 1,        /* tcsc_sgemm_optimized                tcsc.c:101 */
     TCSC_VARIANT_PRELU_BASIC = 2,      /* tcsc_sgemm_prelu_basic              tcsc.c:143 */
     TCSC_VARIANT_PRELU_SEPARATE = 3,   /* tcsc_sgemm_prelu_optimized_separate tcsc.c:179 */
-    TCSC_VARIANT_PRELU_ONTHEGO = 4     /* tcsc_sgemm_prelu_optimized_onthego  tcsc.c:231 */
+    TCSC_VARIANT_PRELU_ONTHEGO = 4,    /* tcsc_sgemm_prelu_optimized_onthego  tcsc.c:231 */
+    TCSC_VARIANT_SPARSE_GEMM = 5       /* sparseGEMM<float>          SparseGEMM.h:104-119:
+                                          y = 0 + sum(+1 rows) - sum(-1 rows); Y = y + b.
+                                          sparseGEMM_PReLU<float> (SparseGEMM.h:151-168)
+                                          is TCSC_VARIANT_PRELU_BASIC: the same order
+                                          as tcsc.c:143-165, the same predicate     */
 };
 
 /* Status codes (0 = success).  HIP errors are passed through as

@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -28,6 +29,7 @@
 #include <vector>
 
 #include "../../include/sparse/tcsc.h"
+#include "../../include/sparse_gemm.h"
 #include "../../include/tcsc_gpu.h"
 #include "tcsc_internal.h"
 
@@ -241,6 +243,12 @@ size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // workspace of one MFMA launch: X3 (M x 3K bf16) + M row flags + "any"
 size_t mfma_ws_bytes(int M, int K) { return align256((size_t)M * 3 * K * 2) + (size_t)(M + 1) * sizeof(int); }
+
+// Variants 0-4 are the tcsc_sgemm_* family (sparse/tcsc.h); 5 is
+// SparseGEMM.h's sparseGEMM<float> (bias last, no activation).  Bias first
+// only for tcsc_sgemm_basic (tcsc.c:74-96).
+bool valid_variant(int v) { return v >= TCSC_VARIANT_BASIC && v <= TCSC_VARIANT_SPARSE_GEMM; }
+bool is_prelu(int v) { return v >= TCSC_VARIANT_PRELU_BASIC && v <= TCSC_VARIANT_PRELU_ONTHEGO; }
 
 bool use_mfma(const tcsc_gpu_plan* p, int M) { return p->w3 && M >= p->mfma_min_M && p->rows > 0; }
 
@@ -589,7 +597,7 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
     }
     if (stage == 1) return TCSC_OK;
     const float one = 1.0f, zero = 0.0f;
-    const bool prelu = variant >= TCSC_VARIANT_PRELU_BASIC;
+    const bool prelu = is_prelu(variant);
     // hipBLASLt, with the bias in its epilogue unless a PReLU pass follows anyway
     LtGemm* g = lt_gemm_for(const_cast<tcsc_gpu_plan*>(p), M, ldy, !prelu);
     bool bias_done = false;
@@ -635,7 +643,7 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
 
 int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy, int variant,
              float a, void* stream, float* ws, size_t ws_bytes, int stage = 0, int force_slices = 0) {
-    if (!p || M < 0 || (stage != 1 && (ldy < p->cols || variant < 0 || variant > 4))) {
+    if (!p || M < 0 || (stage != 1 && (ldy < p->cols || !valid_variant(variant)))) {
         set_error("tcsc_gpu_sgemm: bad arguments (M=%d ldy=%d variant=%d)", M, ldy, variant);
         return TCSC_E_ARG;
     }
@@ -659,7 +667,7 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
             return TCSC_OK;
         }
         HIP_TRY(tcsc::launch_small_m(stage == 2 ? ws : dX, M, p->rows, p->ccp, p->ccn, p->crp, p->crn, p->cols, dB,
-                                     dY, ldy, variant == TCSC_VARIANT_BASIC, variant >= TCSC_VARIANT_PRELU_BASIC, a,
+                                     dY, ldy, variant == TCSC_VARIANT_BASIC, is_prelu(variant), a,
                                      st));
         return TCSC_OK;
     }
@@ -677,9 +685,12 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
     g.sptr = p->sptr;
     g.n_entries = p->n_entries;
     if (p->order == TCSC_ORDER_REFERENCE && p->chain_pos && p->chain_neg) {
-        // basic / prelu_basic: one accumulator, +1 chain then -1 chain;
-        // the optimized family: the two sums apart (k_stream ORDER 2)
-        g.order = (variant == TCSC_VARIANT_BASIC || variant == TCSC_VARIANT_PRELU_BASIC) ? 1 : 2;
+        // basic / prelu_basic / sparseGEMM: one accumulator, +1 chain then
+        // -1 chain; the optimized family: the two sums apart (k_stream ORDER 2)
+        g.order = (variant == TCSC_VARIANT_BASIC || variant == TCSC_VARIANT_PRELU_BASIC ||
+                   variant == TCSC_VARIANT_SPARSE_GEMM)
+                      ? 1
+                      : 2;
         g.ent = p->chain_pos->ent;
         g.sptr = p->chain_pos->sptr;
         g.n_entries = p->chain_pos->n_entries;
@@ -702,7 +713,7 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
     // (tcsc.c:149-161; the optimized family adds per-sign partial sums to
     // the bias, which no single accumulation order reproduces: DESIGN.md).
     g.bias_first = (variant == TCSC_VARIANT_BASIC);
-    g.prelu = (variant >= TCSC_VARIANT_PRELU_BASIC);
+    g.prelu = is_prelu(variant);
     hipError_t e = tcsc::launch_gemm(g, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "tcsc_gpu_sgemm launch");
     return TCSC_OK;
@@ -973,7 +984,7 @@ int tcsc_gpu_from_dense(const float* d_dense, int rows, int cols, int* d_csp, in
 // Y^T (N x M, ld ldy) = W^T (N x K, ld N) * X^T (K x M, ld K).
 int tcsc_gpu_dense_sgemm(const float* dX, const float* dW, const float* dB, float* dY, int M, int N, int K,
                          int ldy, int variant, float a, void* stream) {
-    if (M < 0 || N < 0 || K < 0 || ldy < N || variant < 0 || variant > 4 ||
+    if (M < 0 || N < 0 || K < 0 || ldy < N || !valid_variant(variant) ||
         ((long long)M * N > 0 && (!dX || !dW || !dB || !dY))) {
         set_error("tcsc_gpu_dense_sgemm: bad arguments (M=%d N=%d K=%d ldy=%d variant=%d)", M, N, K, ldy, variant);
         return TCSC_E_ARG;
@@ -1002,7 +1013,7 @@ int tcsc_gpu_dense_sgemm(const float* dX, const float* dW, const float* dB, floa
             return TCSC_E_HIP;
         }
     }
-    HIP_TRY(tcsc::launch_bias_act(dY, M, N, ldy, dB, variant >= TCSC_VARIANT_PRELU_BASIC, a, st));
+    HIP_TRY(tcsc::launch_bias_act(dY, M, N, ldy, dB, is_prelu(variant), a, st));
     return TCSC_OK;
 }
 
@@ -1331,6 +1342,113 @@ void host_sgemm(int variant, const float* X, const tcsc_t* W, const float* B, fl
     report(rc);
 }
 
+// --- SparseGEMM.h's raw-array API (include/sparse_gemm.h) ------------------
+// Its calls carry no tcsc_t, so each distinct col_start_pos array gets a
+// library-owned tcsc_t view; the view goes through host_sgemm like any
+// tcsc_t, so the plan cache's content fingerprint catches arrays that were
+// rebuilt in place or freed and reused.  The reference's harness builds a
+// new SparseFormat per case (SparseGEMM.cpp:101) and never says when one
+// dies, so only the kRawViews most recently used views keep their plans.
+constexpr size_t kRawViews = 8;
+std::mutex g_raw_mu;  // taken before g_mu, never after it
+std::deque<std::pair<const int*, std::unique_ptr<tcsc_t>>> g_raw;  // most recent first
+
+void raw_sgemm(int variant, const float* X, const int* csp, const int* csn, const int* rip, const int* rin,
+               const float* b, float* Y, int M, int N, int K, float a) {
+    if (M <= 0 || N <= 0) return;
+    if (!csp || !csn || K < 0) {
+        set_error("sparseGEMM: NULL col_start array or K=%d", K);
+        report(TCSC_E_ARG);
+        return;
+    }
+    std::lock_guard<std::mutex> rk(g_raw_mu);
+    auto it = std::find_if(g_raw.begin(), g_raw.end(), [&](const auto& e) { return e.first == csp; });
+    std::unique_ptr<tcsc_t> view;
+    if (it != g_raw.end()) {
+        view = std::move(it->second);
+        g_raw.erase(it);
+    } else {
+        view.reset(new tcsc_t{});
+        if (g_raw.size() >= kRawViews) {  // drop the least recently used view and its plans
+            std::lock_guard<std::mutex> lk(g_mu);
+            auto c = g_cache.find(g_raw.back().second.get());
+            if (c != g_cache.end()) {
+                destroy_entry(c->second);
+                g_cache.erase(c);
+            }
+            g_raw.pop_back();
+        }
+    }
+    tcsc_t* v = view.get();
+    g_raw.emplace_front(csp, std::move(view));
+    // the reference's loops run k over [col_start[n], col_start[n+1]) of the
+    // row arrays, so col_start[N] entries of each are addressable
+    v->rows = K;
+    v->cols = N;
+    v->n_elem_pos = csp[N];
+    v->n_elem_neg = csn[N];
+    v->col_start_pos = const_cast<int*>(csp);
+    v->col_start_neg = const_cast<int*>(csn);
+    v->row_index_pos = const_cast<int*>(rip);
+    v->row_index_neg = const_cast<int*>(rin);
+    if ((csp[N] > 0 && !rip) || (csn[N] > 0 && !rin)) {
+        set_error("sparseGEMM: NULL row_index array with %d / %d entries", csp[N], csn[N]);
+        report(TCSC_E_ARG);
+        return;
+    }
+    host_sgemm(variant, X, v, b, a, Y, M, N, K);
+}
+
+// GEMM / GEMM_PReLU (SparseGEMM.h:121-149) on host pointers: the dense
+// baseline through tcsc_gpu_dense_sgemm on the current device, with
+// per-device staging buffers that grow as needed.
+struct DenseStage {
+    float *x = nullptr, *w = nullptr, *b = nullptr, *y = nullptr;
+    size_t x_cap = 0, w_cap = 0, b_cap = 0, y_cap = 0;
+};
+std::vector<DenseStage> g_dense;
+
+void host_dense(int variant, const float* X, const float* W, const float* b, float* Y, int M, int N, int K, float a) {
+    if (M <= 0 || N <= 0) return;
+    if (K < 0 || !Y || !b || (K > 0 && (!X || !W))) {
+        set_error("GEMM: bad arguments (M=%d N=%d K=%d) or NULL", M, N, K);
+        report(TCSC_E_ARG);
+        return;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    const int ndev = device_count_raw();
+    int dev = 0, rc = TCSC_OK;
+    if (ndev <= 0) {
+        set_error("no HIP device visible: GEMM needs a gfx950 GPU");
+        report(TCSC_E_NODEV);
+        return;
+    }
+    if (hipGetDevice(&dev) != hipSuccess || dev >= ndev) dev = 0;
+    if ((int)g_dev.size() < ndev) g_dev.resize(ndev);
+    if ((int)g_dense.size() < ndev) g_dense.resize(ndev);
+    DevState& ds = g_dev[dev];
+    DenseStage& d = g_dense[dev];
+    auto run = [&]() -> int {
+        DeviceGuard dg(dev);
+        if (!ds.stream) HIP_TRY(hipStreamCreateWithFlags(&ds.stream, hipStreamNonBlocking));
+        const size_t xb = (size_t)M * K * sizeof(float), wb = (size_t)K * N * sizeof(float);
+        int r;
+        if ((r = ensure(&d.x, &d.x_cap, xb)) != TCSC_OK || (r = ensure(&d.w, &d.w_cap, wb)) != TCSC_OK ||
+            (r = ensure(&d.b, &d.b_cap, (size_t)N * sizeof(float))) != TCSC_OK ||
+            (r = ensure(&d.y, &d.y_cap, (size_t)M * N * sizeof(float))) != TCSC_OK)
+            return r;
+        if (xb) HIP_TRY(hipMemcpyAsync(d.x, X, xb, hipMemcpyHostToDevice, ds.stream));
+        if (wb) HIP_TRY(hipMemcpyAsync(d.w, W, wb, hipMemcpyHostToDevice, ds.stream));
+        HIP_TRY(hipMemcpyAsync(d.b, b, (size_t)N * sizeof(float), hipMemcpyHostToDevice, ds.stream));
+        if ((r = tcsc_gpu_dense_sgemm(d.x, d.w, d.b, d.y, M, N, K, N, variant, a, ds.stream)) != TCSC_OK) return r;
+        HIP_TRY(hipMemcpyAsync(Y, d.y, (size_t)M * N * sizeof(float), hipMemcpyDeviceToHost, ds.stream));
+        HIP_TRY(hipStreamSynchronize(ds.stream));
+        return TCSC_OK;
+    };
+    rc = run();
+    report(rc);
+}
+
 }  // namespace
 
 namespace tcsc {
@@ -1397,6 +1515,34 @@ void tcsc_free(tcsc_t* W) {
     std::free(W->row_index_pos);
     std::free(W->row_index_neg);
     std::free(W);
+}
+
+}  // extern "C"
+
+// SparseGEMM.h drop-in (include/sparse_gemm.h)
+extern "C" {
+
+void tcsc_sparse_gemm(const float* X, const int* col_start_pos, const int* col_start_neg, const int* row_index_pos,
+                      const int* row_index_neg, const float* b, float* Y, int M, int N, int K) {
+    raw_sgemm(TCSC_VARIANT_SPARSE_GEMM, X, col_start_pos, col_start_neg, row_index_pos, row_index_neg, b, Y, M, N, K,
+              0.0f);
+}
+
+void tcsc_sparse_gemm_prelu(const float* X, const int* col_start_pos, const int* col_start_neg,
+                            const int* row_index_pos, const int* row_index_neg, const float* b, float* Y, int M,
+                            int N, int K, float a) {
+    // y = 0 + sum(+1) - sum(-1); y += b; PReLU (SparseGEMM.h:156-165) is
+    // tcsc_sgemm_prelu_basic's order and predicate (tcsc.c:149-162)
+    raw_sgemm(TCSC_VARIANT_PRELU_BASIC, X, col_start_pos, col_start_neg, row_index_pos, row_index_neg, b, Y, M, N, K,
+              a);
+}
+
+void tcsc_dense_gemm(const float* X, const float* W, const float* b, float* Y, int M, int N, int K) {
+    host_dense(TCSC_VARIANT_SPARSE_GEMM, X, W, b, Y, M, N, K, 0.0f);
+}
+
+void tcsc_dense_gemm_prelu(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, float a) {
+    host_dense(TCSC_VARIANT_PRELU_BASIC, X, W, b, Y, M, N, K, a);
 }
 
 }  // extern "C"

@@ -172,6 +172,53 @@ tcsc_t* tcsc_from_dense(dense_t dense, int rows, int cols) {
     return from_dense_host(dense, rows, cols);
 }
 
+// SparseFormat(int* matrix, int K, int N) (SparseGEMM.h:20-39): an int K x N
+// matrix, >= 1 stored as +1 and <= -1 as -1 (so 2 and -7 count too, unlike
+// tcsc_from_dense's exact compare), rows ascending per column.  Same
+// row-major two-pass walk as from_dense_host; the reference walks column by
+// column with stride N and produces the same arrays.  Two calls: with
+// row_index_* NULL it writes col_start_* (N+1 each) and the counts; then
+// with row_index_* sized n_pos / n_neg it fills them.
+int tcsc_sparse_format(const int* matrix, int K, int N, int* col_start_pos, int* col_start_neg,
+                       int* row_index_pos, int* row_index_neg, int* n_pos, int* n_neg) {
+    if (K < 0 || N < 0 || !col_start_pos || !col_start_neg || (!matrix && (long long)K * N > 0)) return TCSC_E_ARG;
+    std::vector<long long> cnt_p((size_t)N, 0), cnt_n((size_t)N, 0);
+    for (int k = 0; k < K; ++k) {
+        const int* r = matrix + (size_t)k * N;
+        for (int n = 0; n < N; ++n) {
+            cnt_p[n] += (r[n] >= 1);
+            cnt_n[n] += (r[n] <= -1);
+        }
+    }
+    long long p = 0, q = 0;
+    for (int n = 0; n < N; ++n) {
+        col_start_pos[n] = (int)p;
+        col_start_neg[n] = (int)q;
+        p += cnt_p[n];
+        q += cnt_n[n];
+        if (p > 0x7fffffffLL || q > 0x7fffffffLL) return TCSC_E_ARG;
+    }
+    col_start_pos[N] = (int)p;
+    col_start_neg[N] = (int)q;
+    if (n_pos) *n_pos = (int)p;
+    if (n_neg) *n_neg = (int)q;
+    if (!row_index_pos || !row_index_neg) return TCSC_OK;
+    for (int n = 0; n < N; ++n) {  // cursors
+        cnt_p[n] = col_start_pos[n];
+        cnt_n[n] = col_start_neg[n];
+    }
+    for (int k = 0; k < K; ++k) {
+        const int* r = matrix + (size_t)k * N;
+        for (int n = 0; n < N; ++n) {
+            if (r[n] >= 1)
+                row_index_pos[cnt_p[n]++] = k;
+            else if (r[n] <= -1)
+                row_index_neg[cnt_n[n]++] = k;
+        }
+    }
+    return TCSC_OK;
+}
+
 void tcsc_set_seed(unsigned long long seed) { g_seed = seed; }
 
 dense_t init_rand_dense(int rows, int cols) {

@@ -48,6 +48,8 @@ EXPORTED_SYMBOLS = (
     # include/bcsr_gpu.h
     "bcsr_gpu_plan_create", "bcsr_gpu_plan_stats", "bcsr_gpu_plan_reserve", "bcsr_gpu_plan_destroy",
     "bcsr_gpu_sgemm", "bcsr_gpu_prepare_x", "bcsr_gpu_sgemm_prepared",
+    # include/sparse_gemm.h (SparseGEMM.h's raw-array API)
+    "tcsc_sparse_format", "tcsc_sparse_gemm", "tcsc_sparse_gemm_prelu", "tcsc_dense_gemm", "tcsc_dense_gemm_prelu",
 )
 
 
@@ -75,6 +77,7 @@ class plan_info_t(C.Structure):
 
 
 _f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
 _lib = None
 
 
@@ -137,6 +140,17 @@ def lib():
     L.tcsc_gpu_set_order.argtypes = [i]
     L.tcsc_gpu_set_order.restype = None
     L.tcsc_gpu_get_order.restype = i
+    ip = C.POINTER(i)
+    L.tcsc_sparse_format.argtypes = [_i32p, i, i, _i32p, _i32p, vp, vp, ip, ip]
+    L.tcsc_sparse_format.restype = i
+    L.tcsc_sparse_gemm.argtypes = [_f32p, _i32p, _i32p, _i32p, _i32p, _f32p, _f32p, i, i, i]
+    L.tcsc_sparse_gemm.restype = None
+    L.tcsc_sparse_gemm_prelu.argtypes = L.tcsc_sparse_gemm.argtypes + [f]
+    L.tcsc_sparse_gemm_prelu.restype = None
+    L.tcsc_dense_gemm.argtypes = [_f32p, _f32p, _f32p, _f32p, i, i, i]
+    L.tcsc_dense_gemm.restype = None
+    L.tcsc_dense_gemm_prelu.argtypes = L.tcsc_dense_gemm.argtypes + [f]
+    L.tcsc_dense_gemm_prelu.restype = None
     from . import bcsr as _bcsr
 
     _bcsr.bind(L)
@@ -285,6 +299,82 @@ def sgemm(variant: str, X: np.ndarray, W: TcscMatrix, B: np.ndarray, a: float = 
         getattr(L, name)(nz(X), W.ptr, nz(B), a, nz(Y), M, N, K)
     else:
         getattr(L, "tcsc_sgemm_" + variant)(nz(X), W.ptr, nz(B), nz(Y), M, N, K)
+    return Y
+
+
+# --- SparseGEMM.h's raw-array API (include/sparse_gemm.h) -------------------
+
+def sparse_format(matrix: np.ndarray):
+    """SparseFormat(int* matrix, K, N) (SparseGEMM.h:20-39): an int K x N
+    matrix -> (col_start_pos, col_start_neg, row_index_pos, row_index_neg);
+    >= 1 is +1, <= -1 is -1.  Host code in the library (no GPU needed)."""
+    m = np.ascontiguousarray(matrix, dtype=np.int32)
+    if m.ndim != 2:
+        raise TcscError(f"matrix must be 2-D (K x N), got shape {m.shape}")
+    K, N = m.shape
+    flat = m.reshape(-1) if m.size else np.zeros(1, np.int32)
+    csp, csn = np.zeros(N + 1, np.int32), np.zeros(N + 1, np.int32)
+    p, q = C.c_int(0), C.c_int(0)
+    L = lib()
+    _check(L.tcsc_sparse_format(flat, K, N, csp, csn, None, None, C.byref(p), C.byref(q)), "tcsc_sparse_format")
+    rip, rin = np.zeros(max(p.value, 1), np.int32), np.zeros(max(q.value, 1), np.int32)
+    _check(L.tcsc_sparse_format(flat, K, N, csp, csn, rip.ctypes.data, rin.ctypes.data, C.byref(p), C.byref(q)),
+           "tcsc_sparse_format")
+    return csp, csn, rip[:p.value].copy(), rin[:q.value].copy()
+
+
+def sparse_gemm(X: np.ndarray, col_start_pos, col_start_neg, row_index_pos, row_index_neg, b: np.ndarray,
+                a: float | None = None, Y: np.ndarray | None = None) -> np.ndarray:
+    """sparseGEMM<float> (a None) or sparseGEMM_PReLU<float> (SparseGEMM.h:104-119,
+    151-168) on host arrays: Y = act(X . W + b), W given by its four TCSC
+    arrays.  Shapes are checked here (the C entry points trust them)."""
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    if X.ndim != 2:
+        raise TcscError(f"X must be 2-D (M x K), got shape {X.shape}")
+    M, K = X.shape
+    arrs = [np.ascontiguousarray(v, dtype=np.int32).reshape(-1)
+            for v in (col_start_pos, col_start_neg, row_index_pos, row_index_neg)]
+    csp, csn, rip, rin = arrs
+    N = csp.size - 1
+    if N < 0 or csn.size != N + 1:
+        raise TcscError("col_start_pos / col_start_neg must both have N+1 entries")
+    if rip.size < csp[-1] or rin.size < csn[-1]:
+        raise TcscError("row_index arrays shorter than col_start[N]")
+    b = np.ascontiguousarray(b, dtype=np.float32).reshape(-1)
+    if b.size != N:
+        raise TcscError(f"b has {b.size} elements, W has N={N} columns")
+    if Y is None:
+        Y = np.empty((M, N), np.float32)
+    elif Y.shape != (M, N) or Y.dtype != np.float32 or not Y.flags["C_CONTIGUOUS"]:
+        raise TcscError(f"Y must be a C-contiguous float32 array of shape ({M}, {N})")
+    nz = lambda v, t: v if v.size else np.zeros(1, t)  # noqa: E731
+    args = [nz(X.reshape(-1), np.float32), csp, csn, nz(rip, np.int32), nz(rin, np.int32), nz(b, np.float32),
+            nz(Y.reshape(-1), np.float32), M, N, K]
+    if a is None:
+        lib().tcsc_sparse_gemm(*args)
+    else:
+        lib().tcsc_sparse_gemm_prelu(*args, float(a))
+    return Y
+
+
+def dense_gemm(X: np.ndarray, W: np.ndarray, b: np.ndarray, a: float | None = None) -> np.ndarray:
+    """GEMM<float> / GEMM_PReLU<float> (SparseGEMM.h:121-149) on host arrays,
+    computed by the GPU's fp32 rocBLAS product + bias/PReLU epilogue."""
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    W = np.ascontiguousarray(W, dtype=np.float32)
+    if X.ndim != 2 or W.ndim != 2 or X.shape[1] != W.shape[0]:
+        raise TcscError(f"X {X.shape} and W {W.shape} do not chain")
+    M, K = X.shape
+    N = W.shape[1]
+    b = np.ascontiguousarray(b, dtype=np.float32).reshape(-1)
+    if b.size != N:
+        raise TcscError(f"b has {b.size} elements, W has N={N} columns")
+    Y = np.empty((M, N), np.float32)
+    nz = lambda v: v.reshape(-1) if v.size else np.zeros(1, np.float32)  # noqa: E731
+    if a is None:
+        lib().tcsc_dense_gemm(nz(X), nz(W), nz(b), nz(Y), M, N, K)
+    else:
+        lib().tcsc_dense_gemm_prelu(nz(X), nz(W), nz(b), nz(Y), M, N, K, float(a))
     return Y
 
 

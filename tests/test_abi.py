@@ -22,7 +22,7 @@ def built_lib():
 def declared_functions():
     names = set()
     for h in ("include/sparse/tcsc.h", "include/dense/dense.h", "include/tcsc_gpu.h", "include/sparse/bcsr.h",
-              "include/bcsr_gpu.h"):
+              "include/bcsr_gpu.h", "include/sparse_gemm.h"):
         src = open(os.path.join(ROOT, h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         src = re.sub(r"//[^\n]*", "", src)
@@ -57,6 +57,7 @@ HEADER_PROBE = r"""
 #include <tcsc_gpu.h>
 #include <sparse/bcsr.h>
 #include <bcsr_gpu.h>
+#include <sparse_gemm.h>
 typedef void (*gemm_fn)(const dense_t, const tcsc_t *, const dense_t, dense_t, int, int, int);
 typedef void (*prelu_fn)(const dense_t, const tcsc_t *, const dense_t, float, dense_t, int, int, int);
 typedef void (*bgemm_fn)(const dense_t, const bcsr_t, const dense_t, dense_t, int, int, int);
@@ -67,8 +68,12 @@ int main(void) {
                      tcsc_sgemm_prelu_optimized_onthego};
     bgemm_fn bg[3] = {bcsr_sgemm_basic, bcsr_sgemm_avx, bcsr_sgemm_avx2};
     bprelu_fn bp[2] = {bcsr_sgemm_prelu_basic, bcsr_sgemm_prelu_avx};
+    void (*sg)(const float *, const int *, const int *, const int *, const int *, const float *, float *,
+               int, int, int) = tcsc_sparse_gemm;
+    void (*dg)(const float *, const float *, const float *, float *, int, int, int, float) =
+        tcsc_dense_gemm_prelu;
     tcsc_gpu_plan_info info;
-    (void)info; (void)g; (void)p; (void)bg; (void)bp;
+    (void)info; (void)g; (void)p; (void)bg; (void)bp; (void)sg; (void)dg;
     return tcsc_gpu_device_count() < 0;
 }
 """
