@@ -26,6 +26,9 @@ LIB_PATH = os.environ.get("TCSC_AMD_LIB") or os.path.join(PKG_DIR, "lib", "libtc
 
 VARIANTS = ("basic", "optimized", "prelu_basic", "prelu_separate", "prelu_onthego")
 VARIANT_ID = {v: i for i, v in enumerate(VARIANTS)}
+# SparseGEMM.h's sparseGEMM<float> (include/tcsc_gpu.h TCSC_VARIANT_SPARSE_GEMM):
+# bias last, no activation; accepted by the device API (Plan.sgemm)
+VARIANT_ID["sparse_gemm"] = 5
 PRELU_VARIANTS = frozenset(VARIANTS[2:])
 
 # every symbol include/*.h declares (checked by tests/test_abi.py)
@@ -272,7 +275,7 @@ def sgemm(variant: str, X: np.ndarray, W: TcscMatrix, B: np.ndarray, a: float = 
     floats of B and write M rows of pitch N into Y), so the shapes are checked
     here and a mismatch raises :class:`TcscError` instead of reaching the
     library as an out-of-bounds host read or write."""
-    if variant not in VARIANT_ID:
+    if variant not in VARIANTS:
         raise TcscError(f"unknown variant {variant!r} (one of {', '.join(VARIANTS)})")
     if not getattr(W, "ptr", None):
         raise TcscError("W is freed or not a TcscMatrix")

@@ -253,3 +253,44 @@ def test_reference_sparsegemm_harness_passes(gpu):
     assert r.stdout.count("M=") == 27, r.stdout[-2000:]
     assert "not passed" not in r.stdout, r.stdout[-4000:]
     assert r.stdout.count("sGEMM_PReLU cycles=") == 27
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(6))
+def test_raw_api_matches_device_plan_and_oracle(gpu, oracle, seed):
+    """Seeded random shapes: the raw host API (SparseGEMM.h path) against the
+    device API with TCSC_VARIANT_SPARSE_GEMM (bit for bit: same plan, same
+    order) and against the fp64 oracle (bound); integer inputs bit-exact with
+    the oracle's a8 restatement (SparseGEMM.h:104-119)."""
+    import torch
+
+    rng = np.random.default_rng(1000 + seed)
+    M = int(rng.choice([1, 3, 17, 64, 300, 1024]))
+    K = int(rng.integers(1, 3000))
+    N = int(rng.integers(1, 700))
+    dens = float(rng.choice([0.01, 0.05, 0.3]))
+    mat = rng.random((K, N))
+    mat = np.where(mat < dens / 2, 1, np.where(mat < dens, -1, 0)).astype(np.int32)
+    csp, csn, rip, rin = tcsc_amd.sparse_format(mat)
+    W = pyoracle.TCSC(K, N, csp, csn, rip, rin)
+    integer = seed % 2 == 1
+    X = (rng.integers(-512, 513, size=(M, K)) if integer else rng.uniform(-1, 1, size=(M, K))).astype(np.float32)
+    B = (rng.integers(-8, 9, size=N) if integer else rng.uniform(-1, 1, size=N)).astype(np.float32)
+    Y = tcsc_amd.sparse_gemm(X, csp, csn, rip, rin, B)
+    Yp = tcsc_amd.sparse_gemm(X, csp, csn, rip, rin, B, 0.2)
+    Y64, S64 = oracle.f64_rows(X, W, B)
+    assert pyoracle.check_close(Y, Y64, S64)[0]
+    assert pyoracle.check_close(Yp, Y64, S64, 0.2)[0]
+    if integer:
+        _bits(Y, oracle.sparse_gemm_omp(X, W, B, False), "int")
+        _bits(Yp, oracle.sparse_gemm_omp(X, W, B, True, 0.2), "int prelu")
+    dev = torch.device("cuda:0")
+    plan = tcsc_amd.Plan(tcsc_amd.TcscMatrix.from_arrays(K, N, csp, csn, rip, rin))
+    plan.reserve(M)
+    Xd, Bd = torch.from_numpy(X).to(dev), torch.from_numpy(B).to(dev)
+    Yd = torch.empty((M, N), device=dev)
+    for variant, ref in (("sparse_gemm", Y), ("prelu_basic", Yp)):
+        plan.sgemm(Xd, Bd, Yd, M, N, variant, 0.2)
+        torch.cuda.synchronize()
+        _bits(Yd.cpu().numpy(), ref, variant)
+    plan.destroy()
