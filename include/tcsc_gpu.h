@@ -129,6 +129,8 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan *plan);
  *        `cols` are not touched
  *   act: PReLU(v) = (v < 0 ? a*v : v) for the PRELU variants, identity
  *        otherwise.
+ *   M  : at most 2^22 rows per launch on the gather path (TCSC_E_ARG
+ *        beyond; offsets are 64-bit, so M*K may exceed 2^31).
  * Asynchronous on `stream`; once the workspace covers M (see
  * tcsc_gpu_plan_reserve) no allocation and no synchronisation (safe to
  * capture in a hipGraph).

@@ -671,6 +671,13 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
                                      st));
         return TCSC_OK;
     }
+    // gather-path limits: X^T row tiles of 64 rows on the transpose grid's y
+    // axis (<= 65536 blocks) and 32-bit per-lane DMA offsets within a chunk
+    // (kTK rows of ldxt floats): M <= 2^22 rows per launch
+    if (M > (1 << 22)) {
+        set_error("tcsc_gpu_sgemm: M=%d rows in one launch (at most %d; split the rows)", M, 1 << 22);
+        return TCSC_E_ARG;
+    }
     const size_t xtb = tcsc::xt_bytes(M, p->rows);
     if (p->rows > 0 && (!ws || ws_bytes < xtb)) {
         set_error("tcsc_gpu_sgemm: workspace of %zu bytes < %zu needed for M=%d", ws ? ws_bytes : (size_t)0, xtb, M);

@@ -188,3 +188,38 @@ def test_bcsr_prepared_needs_a_staged_x_of_that_shape(gpu, torch_cuda, oracle):
     torch.cuda.synchronize()
     plan.destroy()
     Wb.free()
+
+
+@pytest.mark.parametrize("variant", ["basic", "prelu_onthego"])
+def test_x_beyond_2_31_elements(gpu, torch_cuda, oracle, variant):
+    """Maximum sizes: X with M*K > 2^31 elements (8.6 GB), so every row-major
+    offset m*K + k past row 130,944 and every X^T offset past 2^31 needs 64-bit
+    arithmetic.  Sampled rows on both sides of the crossing against the fp64
+    oracle (the reference's int offsets, tcsc.c:87, would overflow here)."""
+    torch = torch_cuda
+    M, K, N = 131072, 16400, 300
+    assert M * K > 2 ** 31
+    rng = np.random.default_rng(31)
+    dense = rng.random((K, N))
+    dense = np.where(dense < 0.01, 1.0, np.where(dense < 0.02, -1.0, 0.0)).astype(np.float32)
+    W = oracle.tcsc_from_dense(dense)
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(5)
+    X = torch.rand((M, K), device=dev, generator=g) * 2 - 1
+    B = torch.from_numpy(rng.uniform(-1, 1, N).astype(np.float32)).to(dev)
+    Y = torch.empty((M, N), device=dev)
+    lib_w = to_lib(W)
+    plan = tcsc_amd.Plan(lib_w)
+    plan.reserve(M)
+    plan.sgemm(X, B, Y, M, N, variant, 0.2)
+    torch.cuda.synchronize()
+    rows = np.array([0, 1, 65535, 65536, 130943, 130944, 130945, M - 1])
+    idx = torch.from_numpy(rows).to(dev)
+    Xs = X[idx].cpu().numpy()
+    Ys = Y[idx].cpu().numpy()
+    del X
+    plan.destroy()
+    lib_w.free()
+    Y64, S64 = oracle.f64_rows(Xs, W, B.cpu().numpy())
+    ok, worst = pyoracle.check_close(Ys, Y64, S64, 0.2 if variant.startswith("prelu") else None)
+    assert ok, worst
