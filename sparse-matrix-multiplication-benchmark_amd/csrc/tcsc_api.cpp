@@ -15,12 +15,16 @@
 #include <rocblas/rocblas.h>
 
 #include <algorithm>
+#include <array>
+#include <atomic>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -529,22 +533,34 @@ uint64_t fmix64(uint64_t h) {
     return h ^ (h >> 33);
 }
 
+constexpr uint32_t kHashA[4] = {0x9e3779b9u, 0x85ebca6bu, 0xc2b2ae35u, 0x27d4eb2fu};
+constexpr uint32_t kHashB[4] = {0x165667b1u, 0xd3a2646cu, 0xfd7046c5u, 0xb55a4f09u};
+
+// The sums over whole 8-int groups [i0, i1) (multiples of 8) into acc: a sum,
+// so disjoint ranges can be summed on different threads (tcsc_fingerprint_par).
+void hash_groups(const uint32_t* u, long long i0, long long i1, uint64_t acc[4]) {
+    for (long long i = i0; i < i1; i += 8) {
+        const uint32_t pos = (uint32_t)i;
+        for (int j = 0; j < 4; ++j)
+            acc[j] += (uint64_t)(u[i + 2 * j] + kHashA[j] + pos) * (uint64_t)(u[i + 2 * j + 1] + kHashB[j]);
+    }
+}
+
+// The tail (n % 8 ints) and the finalisation, given the groups' sums.
+uint64_t hash_finish(const uint32_t* u, long long n, uint64_t h, uint64_t acc[4]) {
+    for (long long i = n & ~7LL; i < n; ++i)
+        acc[i & 3] += (uint64_t)(u[i] + kHashA[i & 3] + (uint32_t)i) * (uint64_t)(kHashB[i & 3] | 1u);
+    for (int j = 0; j < 4; ++j) h = fmix64(h ^ acc[j]) + (uint64_t)j;
+    return h;
+}
+
 uint64_t hash_ints(const int* p, long long n, uint64_t h) {
     h = fmix64(h ^ (uint64_t)n);
     if (!p || n <= 0) return h;
     const uint32_t* u = reinterpret_cast<const uint32_t*>(p);
-    static constexpr uint32_t kA[4] = {0x9e3779b9u, 0x85ebca6bu, 0xc2b2ae35u, 0x27d4eb2fu};
-    static constexpr uint32_t kB[4] = {0x165667b1u, 0xd3a2646cu, 0xfd7046c5u, 0xb55a4f09u};
     uint64_t acc[4] = {0, 0, 0, 0};
-    long long i = 0;
-    for (; i + 8 <= n; i += 8) {
-        const uint32_t pos = (uint32_t)i;
-        for (int j = 0; j < 4; ++j)
-            acc[j] += (uint64_t)(u[i + 2 * j] + kA[j] + pos) * (uint64_t)(u[i + 2 * j + 1] + kB[j]);
-    }
-    for (; i < n; ++i) acc[i & 3] += (uint64_t)(u[i] + kA[i & 3] + (uint32_t)i) * (uint64_t)(kB[i & 3] | 1u);
-    for (int j = 0; j < 4; ++j) h = fmix64(h ^ acc[j]) + (uint64_t)j;
-    return h;
+    hash_groups(u, 0, n & ~7LL, acc);
+    return hash_finish(u, n, h, acc);
 }
 
 uint64_t tcsc_fingerprint(const tcsc_t* W) {
@@ -1066,13 +1082,157 @@ struct CacheEntry {
 };
 
 // Per-device staging buffers for X, B and Y of the host API, and the copy
-// streams and events of the banded pipeline (run_device).
+// streams, events and pinned host slots of the banded pipeline (run_device).
+constexpr int kPinSlots = 3;
 struct DevState {
     hipStream_t stream = nullptr, s_in = nullptr, s_out = nullptr;
     float *x = nullptr, *b = nullptr, *y = nullptr, *ws = nullptr;
     size_t x_cap = 0, b_cap = 0, y_cap = 0, ws_cap = 0;
-    std::vector<hipEvent_t> ev_in, ev_k;
+    std::vector<hipEvent_t> ev_in, ev_k, ev_out;
+    char* hx[kPinSlots] = {};  // pinned host staging: band b's X in hx[b % kPinSlots]
+    char* hy[kPinSlots] = {};  // and its Y in hy[b % kPinSlots]
+    size_t hx_cap = 0, hy_cap = 0;
 };
+
+// Host copy workers for the pinned staging.  One thread copies pageable
+// memory at 20-29 GB/s, 8 reach ~110-120 GB/s (tools/pcie_bench.cpp on the
+// MI355X box), above the 57 GB/s a PCIe direction takes, so the staging
+// copies keep up with the DMA.  $TCSC_HOST_THREADS sets the count (default
+// 8).  Callers from several threads at once (the pipeline's input and
+// output sides, several devices) share the queue.  The pool is never torn
+// down: its threads sleep on the queue until the process ends.
+class CopyPool {
+  public:
+    explicit CopyPool(int n) {
+        for (int i = 0; i < n; ++i) std::thread([this] { work(); }).detach();
+        n_ = n;
+    }
+    int size() const { return n_; }
+    // rows x row_bytes from src (pitch sp) to dst (pitch dp), split over the
+    // workers; returns once every piece is copied
+    void copy2d(char* dst, size_t dp, const char* src, size_t sp, size_t row_bytes, size_t rows) {
+        if (!rows || !row_bytes) return;
+        if (dp == row_bytes && sp == row_bytes) {  // contiguous: one long row
+            row_bytes *= rows;
+            rows = 1;
+        }
+        std::vector<std::function<void()>> parts;
+        const size_t kMin = 1 << 20;  // pieces of >= 1 MiB
+        if (rows >= (size_t)n_) {
+            for (int t = 0; t < n_; ++t) {
+                const size_t r0 = rows * t / n_, r1 = rows * (t + 1) / n_;
+                parts.push_back([=] {
+                    for (size_t r = r0; r < r1; ++r) std::memcpy(dst + r * dp, src + r * sp, row_bytes);
+                });
+            }
+        } else {
+            const size_t per = std::max(kMin, (row_bytes * rows + n_ - 1) / n_);
+            for (size_t r = 0; r < rows; ++r)
+                for (size_t o = 0; o < row_bytes; o += per) {
+                    const size_t len = std::min(per, row_bytes - o);
+                    parts.push_back([=] { std::memcpy(dst + r * dp + o, src + r * sp + o, len); });
+                }
+        }
+        run(parts);
+    }
+
+    // every function in `parts` on the workers; returns when all are done
+    void run(const std::vector<std::function<void()>>& parts) {
+        struct Done {
+            std::mutex mu;
+            std::condition_variable cv;
+            int left = 0;
+        };
+        auto done = std::make_shared<Done>();  // outlives the last worker's notify
+        done->left = (int)parts.size();
+        if (!done->left) return;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (auto& f : parts)
+                q_.push_back([f, done] {
+                    f();
+                    std::lock_guard<std::mutex> dl(done->mu);
+                    if (--done->left == 0) done->cv.notify_all();
+                });
+        }
+        cv_.notify_all();
+        std::unique_lock<std::mutex> dl(done->mu);
+        done->cv.wait(dl, [&] { return done->left == 0; });
+    }
+
+  private:
+    void work() {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return !q_.empty(); });
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            f();
+        }
+    }
+    int n_ = 0;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+};
+
+// Two pools, one per direction: with one shared FIFO a band's input copy
+// queues behind the previous band's output copy and the pipeline serialises.
+CopyPool& copy_pool(int side) {
+    static CopyPool* pools[2] = {nullptr, nullptr};
+    static std::once_flag once;
+    std::call_once(once, [] {
+        int n = 8;
+        if (const char* e = std::getenv("TCSC_HOST_THREADS")) n = std::max(1, std::min(64, std::atoi(e)));
+        pools[0] = new CopyPool(n);
+        pools[1] = new CopyPool(n);
+    });
+    return *pools[side];
+}
+
+// tcsc_fingerprint with the index arrays' 8-int groups summed on the copy
+// workers (~1 ms serial at cfg 4 on every host call; same value).
+uint64_t tcsc_fingerprint_par(const tcsc_t* W) {
+    const long long kMinPar = 1 << 20;
+    if ((long long)W->n_elem_pos + W->n_elem_neg < kMinPar) return tcsc_fingerprint(W);
+    uint64_t h = fmix64(((uint64_t)(uint32_t)W->rows << 32) | (uint32_t)W->cols);
+    h = hash_ints(W->col_start_pos, (long long)W->cols + 1, h);
+    h = hash_ints(W->col_start_neg, (long long)W->cols + 1, h);
+    CopyPool& pool = copy_pool(0);
+    auto one = [&](const int* p, long long n, uint64_t hh) {
+        hh = fmix64(hh ^ (uint64_t)n);
+        if (!p || n <= 0) return hh;
+        const uint32_t* u = reinterpret_cast<const uint32_t*>(p);
+        const int T = pool.size();
+        const long long groups = n / 8;
+        std::vector<std::array<uint64_t, 4>> part(T, std::array<uint64_t, 4>{0, 0, 0, 0});
+        std::vector<std::function<void()>> fs;
+        for (int t = 0; t < T; ++t)
+            fs.push_back([&, t] { hash_groups(u, 8 * (groups * t / T), 8 * (groups * (t + 1) / T), part[t].data()); });
+        pool.run(fs);
+        uint64_t acc[4] = {0, 0, 0, 0};
+        for (const auto& a : part)
+            for (int j = 0; j < 4; ++j) acc[j] += a[j];
+        return hash_finish(u, n, hh, acc);
+    };
+    h = one(W->row_index_pos, W->n_elem_pos, h);
+    return one(W->row_index_neg, W->n_elem_neg, h);
+}
+
+int ensure_pinned(char* (&slots)[kPinSlots], size_t* cap, size_t bytes) {
+    if (*cap >= bytes && slots[0]) return TCSC_OK;
+    for (auto& p : slots) {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+    }
+    *cap = 0;
+    for (auto& p : slots) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p), bytes, hipHostMallocDefault));
+    *cap = bytes;
+    return TCSC_OK;
+}
 
 std::mutex g_mu;  // guards everything below (host API is re-entrant, not concurrent-fast)
 std::unordered_map<const tcsc_t*, CacheEntry> g_cache;
@@ -1134,7 +1294,7 @@ int get_entry_locked(const tcsc_t* W, CacheEntry** out) {
         return TCSC_E_NODEV;
     }
     if ((int)g_dev.size() < ndev) g_dev.resize(ndev);
-    const uint64_t content = tcsc_fingerprint(W);
+    const uint64_t content = tcsc_fingerprint_par(W);
     auto it = g_cache.find(W);
     if (it != g_cache.end()) {
         if (fingerprint_matches(it->second, W, content)) {
@@ -1189,30 +1349,161 @@ struct Job {
     int m0, m1;
 };
 
-// Row bands of one job for the copy/compute pipeline: X arrives from pageable
-// host memory at ~50 GB/s, so at cfg 4 the H2D of X and the D2H of Y take
-// ~10 ms against 1.3 ms of kernels.  Split into bands (whole 256-row tiles,
-// >= 32 MB of X each, at most 8), band b's kernels run while band b+1's X
-// and band b-1's Y cross PCIe.  Only on the gather path with the split-K
-// factor of the whole job forced on every band: each element is then summed
-// in the same order as by one launch, so the bits do not change.
-// TCSC_HOST_BANDS=1 turns the pipeline off, =n asks for n bands.
+// Row bands of one job for the copy/compute pipeline (run_bands): X arrives
+// from pageable host memory and Y goes back to it, ~10 ms of PCIe at cfg 4
+// against 1.3 ms of kernels.  Split into bands (whole 256-row tiles), band
+// b's kernels run while band b+1's X and band b-1's Y cross PCIe in both
+// directions.  Measured (tools/host_pipe_sweep.py, 8 copy workers per
+// direction): 8-16 bands are best from 64 MB of X up (cfg 4: 11.1 -> 7.4 ms;
+// 2048x8192: 3.0 -> 2.3 ms); below ~48 MB the single-shot pageable copies
+// win (cfg 2: 0.82 ms against 0.86-1.0 banded).  Only on the gather path
+// with the split-K factor of the whole job forced on every band: each
+// element is then summed in the same order as by one launch, so the bits
+// do not change.  TCSC_HOST_BANDS=1 turns the pipeline off, =n asks for n.
 int host_bands(const tcsc_gpu_plan* p, int M, int K) {
     if (use_mfma(p, M) || use_small(p, M) || K <= 0) return 1;
-    const double xbytes = (double)M * K * sizeof(float);
-    int nb = (int)(xbytes / (32.0 * 1024 * 1024));
-    if (const char* e = std::getenv("TCSC_HOST_BANDS")) nb = std::atoi(e);
-    nb = std::min(nb, 8);
+    const double xbytes = (double)M * K * sizeof(float), MiB = 1024.0 * 1024;
+    int nb = xbytes < 48 * MiB ? 1 : std::max(4, std::min(16, (int)(xbytes / (8 * MiB))));
+    if (const char* e = std::getenv("TCSC_HOST_BANDS")) nb = std::min(std::atoi(e), 16);
     nb = std::min(nb, M / tcsc::kTM);  // whole row tiles
     return nb < 2 ? 1 : nb;
 }
 
-int ensure_events(std::vector<hipEvent_t>& v, size_t n) {
+int ensure_events(std::vector<hipEvent_t>& v, size_t n, unsigned flags = hipEventDisableTiming) {
     while (v.size() < n) {
         hipEvent_t e;
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e, flags));
         v.push_back(e);
     }
+    return TCSC_OK;
+}
+
+// One large job as a pipeline of row bands (host_bands) through pinned host
+// slots.  Pageable copies reach ~56 GB/s for H2D and D2H together, because
+// the runtime stages them through its own buffers one direction at a time;
+// pinned copies run both directions at once (97 GB/s, tools/pcie_bench.cpp).
+// So band b's X goes pageable -> hx[b % 3] on the copy workers, then H2D on
+// s_in; the kernels run on the compute stream; its Y goes D2H into
+// hy[b % 3] on s_out, and an output thread moves it into the caller's Y
+// while the next bands are in flight.  The input side reuses an X slot once
+// its H2D is done (ev_in); it reuses a Y slot once the output thread has
+// drained it (`drained`).  Every band runs with the split-K factor of the
+// whole job, so the bits equal one launch's.
+int run_bands(int dev, DevState& ds, const Shard& sh, int m0, int M, int nb, const float* X, const float* B, float* Y,
+              int N, int K, int variant, float a) {
+    const tcsc_gpu_plan* p = sh.plan;
+    const int nc = sh.c1 - sh.c0;
+    hipStream_t st = ds.stream;
+    int rc;
+    const int s = tcsc::choose_slices(M, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
+                                      slices_override());
+    const int rows_per = (M + nb - 1) / nb;
+    const int bm = (rows_per + tcsc::kTM - 1) / tcsc::kTM * tcsc::kTM;
+    const int nbands = (M + bm - 1) / bm;
+    const size_t xrow = (size_t)K * sizeof(float), yrow = (size_t)nc * sizeof(float);
+    const size_t wsb = tcsc::xt_bytes(bm, K) + tcsc::workspace_bytes(bm, nc, s);
+    if ((rc = ensure(&ds.x, &ds.x_cap, (size_t)M * xrow)) != TCSC_OK) return rc;
+    if ((rc = ensure(&ds.ws, &ds.ws_cap, wsb)) != TCSC_OK) return rc;
+    if ((rc = ensure_pinned(ds.hx, &ds.hx_cap, (size_t)bm * xrow)) != TCSC_OK) return rc;
+    if ((rc = ensure_pinned(ds.hy, &ds.hy_cap, (size_t)bm * yrow)) != TCSC_OK) return rc;
+    if (!ds.s_in) HIP_TRY(hipStreamCreateWithFlags(&ds.s_in, hipStreamNonBlocking));
+    if (!ds.s_out) HIP_TRY(hipStreamCreateWithFlags(&ds.s_out, hipStreamNonBlocking));
+    // the host waits on ev_in / ev_out sleep instead of spinning next to the copy workers
+    const unsigned host_wait = hipEventDisableTiming | hipEventBlockingSync;
+    if ((rc = ensure_events(ds.ev_in, nbands, host_wait)) != TCSC_OK ||
+        (rc = ensure_events(ds.ev_k, nbands)) != TCSC_OK || (rc = ensure_events(ds.ev_out, nbands, host_wait)) != TCSC_OK)
+        return rc;
+    HIP_TRY(hipMemcpyAsync(ds.b, B + sh.c0, yrow, hipMemcpyHostToDevice, st));
+    CopyPool& pool_in = copy_pool(0);
+    CopyPool& pool_out = copy_pool(1);
+    auto band = [&](int b, int* r0, int* r1) {
+        *r0 = b * bm;
+        *r1 = std::min(M, *r0 + bm);
+    };
+
+    // output side: band by band, wait for its D2H, copy it into Y's rows/columns
+    std::mutex mu;
+    std::condition_variable cv;
+    int drained = 0, enqueued = 0;  // bands copied out / bands whose D2H is enqueued
+    bool stop = false;
+    int out_rc = TCSC_OK;
+    std::string out_err;
+    std::thread out([&] {
+        for (int b = 0; b < nbands; ++b) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return enqueued > b || stop; });
+                if (enqueued <= b) return;
+            }
+            const hipError_t e = hipEventSynchronize(ds.ev_out[b]);
+            if (e != hipSuccess) {
+                out_rc = hip_fail(e, "hipEventSynchronize (band D2H)");
+                out_err = g_last_error;
+                std::lock_guard<std::mutex> lk(mu);
+                drained = nbands;  // unblock the input side
+                cv.notify_all();
+                return;
+            }
+            int r0, r1;
+            band(b, &r0, &r1);
+            pool_out.copy2d(reinterpret_cast<char*>(Y + (size_t)(m0 + r0) * N + sh.c0), (size_t)N * sizeof(float),
+                        ds.hy[b % kPinSlots], yrow, yrow, (size_t)(r1 - r0));
+            std::lock_guard<std::mutex> lk(mu);
+            drained = b + 1;
+            cv.notify_all();
+        }
+    });
+    auto finish = [&](int r) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        out.join();
+        if (r == TCSC_OK && out_rc != TCSC_OK) {
+            g_last_error = out_err;
+            return out_rc;
+        }
+        return r;
+    };
+
+    // input side
+    for (int b = 0; b < nbands; ++b) {
+        const int slot = b % kPinSlots;
+        int r0, r1;
+        band(b, &r0, &r1);
+        const hipError_t e = b >= kPinSlots ? hipEventSynchronize(ds.ev_in[b - kPinSlots]) : hipSuccess;
+        if (e != hipSuccess) return finish(hip_fail(e, "hipEventSynchronize (band H2D)"));
+        pool_in.copy2d(ds.hx[slot], xrow, reinterpret_cast<const char*>(X + (size_t)(m0 + r0) * K), xrow, xrow,
+                    (size_t)(r1 - r0));
+        float* xb = ds.x + (size_t)r0 * K;
+        hipError_t he = hipMemcpyAsync(xb, ds.hx[slot], (size_t)(r1 - r0) * xrow, hipMemcpyHostToDevice, ds.s_in);
+        if (he == hipSuccess) he = hipEventRecord(ds.ev_in[b], ds.s_in);
+        if (he == hipSuccess) he = hipStreamWaitEvent(st, ds.ev_in[b], 0);
+        if (he != hipSuccess) return finish(hip_fail(he, "band H2D"));
+        if ((rc = sgemm_ws(p, xb, ds.b, ds.y + (size_t)r0 * nc, r1 - r0, nc, variant, a, st, ds.ws, ds.ws_cap, 0,
+                           s)) != TCSC_OK)
+            return finish(rc);
+        he = hipEventRecord(ds.ev_k[b], st);
+        if (he == hipSuccess) he = hipStreamWaitEvent(ds.s_out, ds.ev_k[b], 0);
+        if (he != hipSuccess) return finish(hip_fail(he, "band kernels"));
+        {  // the Y slot must have been copied out (band b - kPinSlots)
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return drained >= b - kPinSlots + 1; });
+        }
+        he = hipMemcpyAsync(ds.hy[slot], ds.y + (size_t)r0 * nc, (size_t)(r1 - r0) * yrow, hipMemcpyDeviceToHost,
+                            ds.s_out);
+        if (he == hipSuccess) he = hipEventRecord(ds.ev_out[b], ds.s_out);
+        if (he != hipSuccess) return finish(hip_fail(he, "band D2H"));
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            enqueued = b + 1;
+        }
+        cv.notify_all();
+    }
+    rc = finish(TCSC_OK);
+    if (rc != TCSC_OK) return rc;
+    HIP_TRY(hipStreamSynchronize(st));
     return TCSC_OK;
 }
 
@@ -1234,44 +1525,7 @@ int run_device(int dev, const std::vector<Job>& jobs, const float* X, const floa
         if ((rc = ensure(&ds.b, &ds.b_cap, (size_t)nc * sizeof(float))) != TCSC_OK) return rc;
         if ((rc = ensure(&ds.y, &ds.y_cap, (size_t)M * nc * sizeof(float))) != TCSC_OK) return rc;
         if (nb > 1) {
-            const tcsc_gpu_plan* p = sh->plan;
-            const int s = tcsc::choose_slices(M, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
-                                              slices_override());
-            const int rows_per = (M + nb - 1) / nb;
-            const int bm = (rows_per + tcsc::kTM - 1) / tcsc::kTM * tcsc::kTM;
-            const size_t wsb = tcsc::xt_bytes(bm, K) + tcsc::workspace_bytes(bm, nc, s);
-            if ((rc = ensure(&ds.x, &ds.x_cap, (size_t)M * K * sizeof(float))) != TCSC_OK) return rc;
-            if ((rc = ensure(&ds.ws, &ds.ws_cap, wsb)) != TCSC_OK) return rc;
-            if (!ds.s_in) HIP_TRY(hipStreamCreateWithFlags(&ds.s_in, hipStreamNonBlocking));
-            if (!ds.s_out) HIP_TRY(hipStreamCreateWithFlags(&ds.s_out, hipStreamNonBlocking));
-            if ((rc = ensure_events(ds.ev_in, nb)) != TCSC_OK || (rc = ensure_events(ds.ev_k, nb)) != TCSC_OK)
-                return rc;
-            HIP_TRY(hipMemcpyAsync(ds.b, B + sh->c0, (size_t)nc * sizeof(float), hipMemcpyHostToDevice, st));
-            auto d2h = [&](int b) -> int {
-                const int r0 = b * bm, r1 = std::min(M, r0 + bm);
-                HIP_TRY(hipStreamWaitEvent(ds.s_out, ds.ev_k[b], 0));
-                HIP_TRY(hipMemcpy2DAsync(Y + (size_t)(j.m0 + r0) * N + sh->c0, (size_t)N * sizeof(float),
-                                         ds.y + (size_t)r0 * nc, (size_t)nc * sizeof(float),
-                                         (size_t)nc * sizeof(float), r1 - r0, hipMemcpyDeviceToHost, ds.s_out));
-                return TCSC_OK;
-            };
-            int nbands = 0;
-            for (int b = 0; b * bm < M; ++b, ++nbands) {
-                const int r0 = b * bm, r1 = std::min(M, r0 + bm);
-                float* xb = ds.x + (size_t)r0 * K;
-                HIP_TRY(hipMemcpyAsync(xb, X + (size_t)(j.m0 + r0) * K, (size_t)(r1 - r0) * K * sizeof(float),
-                                       hipMemcpyHostToDevice, ds.s_in));
-                HIP_TRY(hipEventRecord(ds.ev_in[b], ds.s_in));
-                HIP_TRY(hipStreamWaitEvent(st, ds.ev_in[b], 0));
-                if ((rc = sgemm_ws(p, xb, ds.b, ds.y + (size_t)r0 * nc, r1 - r0, nc, variant, a, st, ds.ws,
-                                   ds.ws_cap, 0, s)) != TCSC_OK)
-                    return rc;
-                HIP_TRY(hipEventRecord(ds.ev_k[b], st));
-                if (b > 0 && (rc = d2h(b - 1)) != TCSC_OK) return rc;
-            }
-            if ((rc = d2h(nbands - 1)) != TCSC_OK) return rc;
-            HIP_TRY(hipStreamSynchronize(ds.s_out));
-            HIP_TRY(hipStreamSynchronize(st));
+            if ((rc = run_bands(dev, ds, *j.sh, j.m0, M, nb, X, B, Y, N, K, variant, a)) != TCSC_OK) return rc;
             staged0 = j.m0;
             staged1 = j.m1;
             continue;

@@ -376,3 +376,30 @@ def test_split_k_paths(gpu, torch_cuda, oracle, monkeypatch, slices):
     Yh = tcsc_amd.sgemm("basic", Xi, Wm, Bi)
     np.testing.assert_array_equal(Yh, oracle.sgemm("basic", Xi, W, Bi))
     plan.destroy()
+
+
+@pytest.mark.parametrize("axis,shards,bands", [("cols", 2, 3), ("cols", 3, 4), ("rows", 2, 2)])
+def test_host_bands_with_blocks_bit_identical(gpu, oracle, axis, shards, bands, monkeypatch):
+    """The pinned-staging band pipeline under the host API's blocks: column
+    blocks copy each band's Y out with Y's row pitch (the first block stages X
+    in bands, the next ones reuse it), row blocks band each block's rows.
+    Bits equal the same blocks without the pipeline (TCSC_HOST_BANDS=1: one
+    pageable copy each way); within the bound of the exact sums."""
+    M, K, N = 1300, 900, 520
+    Wd = oracle.ternary((K, N), 0.05, 801)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    X, B = oracle.uniform((M, K), 802), oracle.uniform((N,), 803)
+    monkeypatch.setenv("TCSC_SHARD_AXIS", axis)
+    tcsc_amd.set_num_shards(shards)
+    try:
+        monkeypatch.setenv("TCSC_HOST_BANDS", "1")
+        Y1 = tcsc_amd.sgemm("prelu_separate", X, W, B, 0.2)
+        monkeypatch.setenv("TCSC_HOST_BANDS", str(bands))
+        for _ in range(2):  # a second call reuses the pinned slots and the cached plans
+            Yh = tcsc_amd.sgemm("prelu_separate", X, W, B, 0.2)
+            np.testing.assert_array_equal(Yh.view(np.uint32), Y1.view(np.uint32))
+    finally:
+        tcsc_amd.set_num_shards(0)
+    Y64, S64 = oracle.f64_rows(X, oracle.tcsc_from_dense(Wd), B)
+    assert pyoracle.check_close(Yh, Y64, S64, 0.2)[0]
+    W.free()
