@@ -350,7 +350,7 @@ def host_api_line(tcsc_amd, cfg, ncols, variant, X, B, Y, csp, csn, rip, rin, ad
             "first_call_ms": first * 1e3, "calls": calls,
             "pcie_bytes": 4 * (cfg.M * cfg.K + cfg.M * ncols + ncols),
             "bit_identical_to_device_api": same,
-            "note": "pageable host X/B/Y; H2D + kernels + D2H, row bands pipelined over 3 streams"}
+            "note": "pageable host X/B/Y; H2D + kernels + D2H, row bands through pinned slots over 3 streams"}
 
 
 def other_configs(tcsc_amd, workloads, dev, sh, timed, skip):
