@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <atomic>
 #include <condition_variable>
 #include <cstdarg>
@@ -1414,6 +1415,11 @@ int run_bands(int dev, DevState& ds, const Shard& sh, int m0, int M, int nb, con
         (rc = ensure_events(ds.ev_k, nbands)) != TCSC_OK || (rc = ensure_events(ds.ev_out, nbands, host_wait)) != TCSC_OK)
         return rc;
     HIP_TRY(hipMemcpyAsync(ds.b, B + sh.c0, yrow, hipMemcpyHostToDevice, st));
+    // $TCSC_HOST_TRACE: per-band timeline on stderr (ms since the call entered run_bands)
+    static const bool trace = std::getenv("TCSC_HOST_TRACE") != nullptr;
+    const auto T0 = std::chrono::steady_clock::now();
+    auto now_ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count(); };
+    std::vector<double> t_in0(nbands), t_in1(nbands), t_out0(nbands), t_out1(nbands), t_wy(nbands);
     CopyPool& pool_in = copy_pool(0);
     CopyPool& pool_out = copy_pool(1);
     auto band = [&](int b, int* r0, int* r1) {
@@ -1446,8 +1452,10 @@ int run_bands(int dev, DevState& ds, const Shard& sh, int m0, int M, int nb, con
             }
             int r0, r1;
             band(b, &r0, &r1);
+            t_out0[b] = now_ms();
             pool_out.copy2d(reinterpret_cast<char*>(Y + (size_t)(m0 + r0) * N + sh.c0), (size_t)N * sizeof(float),
                         ds.hy[b % kPinSlots], yrow, yrow, (size_t)(r1 - r0));
+            t_out1[b] = now_ms();
             std::lock_guard<std::mutex> lk(mu);
             drained = b + 1;
             cv.notify_all();
@@ -1474,8 +1482,10 @@ int run_bands(int dev, DevState& ds, const Shard& sh, int m0, int M, int nb, con
         band(b, &r0, &r1);
         const hipError_t e = b >= kPinSlots ? hipEventSynchronize(ds.ev_in[b - kPinSlots]) : hipSuccess;
         if (e != hipSuccess) return finish(hip_fail(e, "hipEventSynchronize (band H2D)"));
+        t_in0[b] = now_ms();
         pool_in.copy2d(ds.hx[slot], xrow, reinterpret_cast<const char*>(X + (size_t)(m0 + r0) * K), xrow, xrow,
                     (size_t)(r1 - r0));
+        t_in1[b] = now_ms();
         float* xb = ds.x + (size_t)r0 * K;
         hipError_t he = hipMemcpyAsync(xb, ds.hx[slot], (size_t)(r1 - r0) * xrow, hipMemcpyHostToDevice, ds.s_in);
         if (he == hipSuccess) he = hipEventRecord(ds.ev_in[b], ds.s_in);
@@ -1491,6 +1501,7 @@ int run_bands(int dev, DevState& ds, const Shard& sh, int m0, int M, int nb, con
             std::unique_lock<std::mutex> lk(mu);
             cv.wait(lk, [&] { return drained >= b - kPinSlots + 1; });
         }
+        t_wy[b] = now_ms();
         he = hipMemcpyAsync(ds.hy[slot], ds.y + (size_t)r0 * nc, (size_t)(r1 - r0) * yrow, hipMemcpyDeviceToHost,
                             ds.s_out);
         if (he == hipSuccess) he = hipEventRecord(ds.ev_out[b], ds.s_out);
@@ -1502,6 +1513,12 @@ int run_bands(int dev, DevState& ds, const Shard& sh, int m0, int M, int nb, con
         cv.notify_all();
     }
     rc = finish(TCSC_OK);
+    if (trace) {
+        for (int b = 0; b < nbands; ++b)
+            std::fprintf(stderr, "[tcsc_amd] band %d: X copy %.3f-%.3f, D2H enqueued %.3f, Y copy %.3f-%.3f ms\n", b,
+                         t_in0[b], t_in1[b], t_wy[b], t_out0[b], t_out1[b]);
+        std::fprintf(stderr, "[tcsc_amd] bands done %.3f ms\n", now_ms());
+    }
     if (rc != TCSC_OK) return rc;
     HIP_TRY(hipStreamSynchronize(st));
     return TCSC_OK;
