@@ -1355,17 +1355,19 @@ struct Job {
 // against 1.3 ms of kernels.  Split into bands (whole 256-row tiles), band
 // b's kernels run while band b+1's X and band b-1's Y cross PCIe in both
 // directions.  Measured (tools/host_pipe_sweep.py, 8 copy workers per
-// direction): 8-16 bands are best from 64 MB of X up (cfg 4: 11.1 -> 7.4 ms;
-// 2048x8192: 3.0 -> 2.3 ms); below ~48 MB the single-shot pageable copies
-// win (cfg 2: 0.82 ms against 0.86-1.0 banded).  Only on the gather path
+// direction): 8 bands are best from 64 MB of X up (cfg 4: 11.1 -> 7.4-8.4 ms
+// through torch's HIP runtime, 11.2 -> 9.2 ms in the native driver, where 16
+// bands of 16 MB lose the H2D/D2H overlap again; 2048x8192: 3.0 -> 2.3 ms);
+// below ~48 MB the single-shot pageable copies win (cfg 2: 0.82 ms against
+// 0.86-1.0 banded).  Only on the gather path
 // with the split-K factor of the whole job forced on every band: each
 // element is then summed in the same order as by one launch, so the bits
 // do not change.  TCSC_HOST_BANDS=1 turns the pipeline off, =n asks for n.
 int host_bands(const tcsc_gpu_plan* p, int M, int K) {
     if (use_mfma(p, M) || use_small(p, M) || K <= 0) return 1;
     const double xbytes = (double)M * K * sizeof(float), MiB = 1024.0 * 1024;
-    int nb = xbytes < 48 * MiB ? 1 : std::max(4, std::min(16, (int)(xbytes / (8 * MiB))));
-    if (const char* e = std::getenv("TCSC_HOST_BANDS")) nb = std::min(std::atoi(e), 16);
+    int nb = xbytes < 48 * MiB ? 1 : std::max(4, std::min(8, (int)(xbytes / (8 * MiB))));
+    if (const char* e = std::getenv("TCSC_HOST_BANDS")) nb = std::min(std::atoi(e), 64);
     nb = std::min(nb, M / tcsc::kTM);  // whole row tiles
     return nb < 2 ? 1 : nb;
 }
