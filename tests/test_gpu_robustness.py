@@ -147,6 +147,34 @@ def test_cache_sees_arrays_rebuilt_in_place(gpu, oracle):
     Wl.free()
 
 
+@pytest.mark.parametrize("where", ["first", "last"])
+def test_cache_sees_one_changed_index_in_a_large_matrix(gpu, oracle, where):
+    """Past 2^20 nonzeros the fingerprint is summed on the copy workers in
+    slices: a single row index changed in place, in the first or the last
+    slice, must still give a fresh plan."""
+    M, K, N = 8, 8192, 8192
+    W = oracle.tcsc_from_dense(oracle.ternary((K, N), 0.02, 71))
+    assert W.row_index_pos.size + W.row_index_neg.size > 2 ** 20
+    Wl = to_lib(W)
+    Xi = oracle.integers((M, K), 72)
+    Bi = oracle.integers((N,), 73)
+    np.testing.assert_array_equal(tcsc_amd.sgemm("basic", Xi, Wl, Bi), oracle.sgemm("basic", Xi, W, Bi))
+    rin = Wl.row_index("neg")
+    cs = W.col_start_neg
+    col = 0 if where == "first" else N - 1
+    while cs[col + 1] == cs[col]:
+        col += 1 if where == "first" else -1
+    j = cs[col] if where == "first" else cs[col + 1] - 1
+    lo = rin[j - 1] + 1 if j > cs[col] else 0  # keep the column ascending
+    hi = rin[j + 1] - 1 if j + 1 < cs[col + 1] else K - 1
+    new = lo if rin[j] != lo else hi
+    assert new != rin[j]
+    rin[j] = new
+    W2 = pyoracle.TCSC(K, N, W.col_start_pos, cs, W.row_index_pos, rin.copy())
+    np.testing.assert_array_equal(tcsc_amd.sgemm("basic", Xi, Wl, Bi), oracle.sgemm("basic", Xi, W2, Bi))
+    Wl.free()
+
+
 def test_prepared_needs_a_staged_x_of_that_m(gpu, torch_cuda, oracle):
     torch = torch_cuda
     dev = torch.device("cuda:0")
