@@ -1392,6 +1392,7 @@ int ensure_events(std::vector<hipEvent_t>& v, size_t n, unsigned flags = hipEven
 // its H2D is done (ev_in); it reuses a Y slot once the output thread has
 // drained it (`drained`).  Every band runs with the split-K factor of the
 // whole job, so the bits equal one launch's.
+constexpr int kNoPinned = -1;  // run_bands: no pinned slots, take the unbanded path
 int run_bands(int dev, DevState& ds, const Shard& sh, int m0, int M, int nb, const float* X, const float* B, float* Y,
               int N, int K, int variant, float a) {
     const tcsc_gpu_plan* p = sh.plan;
@@ -1407,8 +1408,14 @@ int run_bands(int dev, DevState& ds, const Shard& sh, int m0, int M, int nb, con
     const size_t wsb = tcsc::xt_bytes(bm, K) + tcsc::workspace_bytes(bm, nc, s);
     if ((rc = ensure(&ds.x, &ds.x_cap, (size_t)M * xrow)) != TCSC_OK) return rc;
     if ((rc = ensure(&ds.ws, &ds.ws_cap, wsb)) != TCSC_OK) return rc;
-    if ((rc = ensure_pinned(ds.hx, &ds.hx_cap, (size_t)bm * xrow)) != TCSC_OK) return rc;
-    if ((rc = ensure_pinned(ds.hy, &ds.hy_cap, (size_t)bm * yrow)) != TCSC_OK) return rc;
+    if (ensure_pinned(ds.hx, &ds.hx_cap, (size_t)bm * xrow) != TCSC_OK ||
+        ensure_pinned(ds.hy, &ds.hy_cap, (size_t)bm * yrow) != TCSC_OK) {
+        // no pinned memory to be had (a locked-memory limit): the caller
+        // takes the single-copy path instead, with the same bits
+        (void)hipGetLastError();
+        g_last_error.clear();
+        return kNoPinned;
+    }
     if (!ds.s_in) HIP_TRY(hipStreamCreateWithFlags(&ds.s_in, hipStreamNonBlocking));
     if (!ds.s_out) HIP_TRY(hipStreamCreateWithFlags(&ds.s_out, hipStreamNonBlocking));
     // the host waits on ev_in / ev_out sleep instead of spinning next to the copy workers
@@ -1544,10 +1551,13 @@ int run_device(int dev, const std::vector<Job>& jobs, const float* X, const floa
         if ((rc = ensure(&ds.b, &ds.b_cap, (size_t)nc * sizeof(float))) != TCSC_OK) return rc;
         if ((rc = ensure(&ds.y, &ds.y_cap, (size_t)M * nc * sizeof(float))) != TCSC_OK) return rc;
         if (nb > 1) {
-            if ((rc = run_bands(dev, ds, *j.sh, j.m0, M, nb, X, B, Y, N, K, variant, a)) != TCSC_OK) return rc;
-            staged0 = j.m0;
-            staged1 = j.m1;
-            continue;
+            rc = run_bands(dev, ds, *j.sh, j.m0, M, nb, X, B, Y, N, K, variant, a);
+            if (rc == TCSC_OK) {
+                staged0 = j.m0;
+                staged1 = j.m1;
+                continue;
+            }
+            if (rc != kNoPinned) return rc;
         }
         if (j.m0 != staged0 || j.m1 != staged1) {
             const size_t xb = (size_t)M * K * sizeof(float);
