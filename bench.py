@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--no-other-configs", action="store_true",
                    help="skip the other BASELINE configs' timings (N=1 only)")
     p.add_argument("--no-validate", action="store_true", help="skip the pre-timing check against the dense product")
+    p.add_argument("--no-graph", action="store_true",
+                   help="skip the HIP-graph line (the same steps captured once and replayed; N=1 only)")
     p.add_argument("--no-host-api", action="store_true",
                    help="skip the drop-in host-pointer call line (PCIe included; N=1 only)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -314,6 +316,10 @@ def main():
                 ref[v] = {"ms": t * 1e3, "g_add_ops_per_s": adds_per_launch / t / 1e9, "vs_fast_order": t / gather_s}
             rplan.destroy()
             out["reference_order"] = ref
+        if world == 1 and not args.no_graph:
+            # the same K steps captured in one HIP graph and replayed (not `value`): what the
+            # launch gaps between k_transpose and k_stream cost on the eager stream
+            out["graph"] = graph_line(plan, X, B, Y, cfg.M, ncols, variant, args.steps, stream, elapsed_max)
         if world == 1 and not args.no_other_configs and not args.override:
             out["other_configs"] = other_configs(tcsc_amd, workloads, dev, sh, timed, cfg.idx)
         if world == 1 and not args.no_cpu_baseline:
@@ -444,6 +450,32 @@ def check_determinism(step, Y, n):
     if not same:
         raise SystemExit(f"validation failed: output changed over {n} identical launches")
     return {"launches": n, "bit_identical": same}
+
+
+def graph_line(plan, X, B, Y, M, ncols, variant, steps, stream, eager_s):
+    """`steps` launches of the step captured in one HIP graph (include/tcsc_gpu.h:
+    a launch whose workspace is reserved allocates nothing and never synchronises),
+    replayed after one warm-up replay; HIP events around the replay."""
+    import torch
+
+    side = torch.cuda.Stream(device=X.device)
+    side.wait_stream(stream)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        h = torch.cuda.current_stream().cuda_stream
+        for _ in range(steps):
+            plan.sgemm(X, B, Y, M, ncols, variant, 0.2, h)
+    g.replay()  # on torch's current stream
+    torch.cuda.synchronize()
+    cur = torch.cuda.current_stream(X.device)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(cur)
+    g.replay()
+    b.record(cur)
+    b.synchronize()
+    ms = a.elapsed_time(b) / steps
+    del g
+    return {"steps_per_graph": steps, "ms_per_step": ms, "vs_eager": ms / (eager_s / steps * 1e3)}
 
 
 def bcsr_line(cfg, Wd, X, B, Y, nnz, tcsc_s, timed, sh, n):
