@@ -301,10 +301,18 @@ __device__ __forceinline__ void gather_stream(i32x16 (&sb)[TCSC_SBUF_VECS], sbuf
                                               unsigned long long& ptr, unsigned lane, unsigned mask,
                                               f32x32 (&acc)[TCSC_ACC_VECS]) {
     (void)sbt;
+#if defined(TCSC_GEN_PF) && TCSC_GEN_PF
+    int junk = 0;  // destination of the reload prefetch (tools/gen_gather_asm.py --pf)
+    asm volatile(TCSC_GATHER_ASM
+                 : TCSC_ACC_OPERANDS(acc), TCSC_SBUF_OPERANDS(sb, sbt), TCSC_PTR_OPERAND(ptr), TCSC_JUNK_OPERAND(junk)
+                 : [lane] "v"(lane * 16u), [mask] "v"(mask)
+                 : TCSC_GATHER_CLOBBERS);
+#else
     asm volatile(TCSC_GATHER_ASM
                  : TCSC_ACC_OPERANDS(acc), TCSC_SBUF_OPERANDS(sb, sbt), TCSC_PTR_OPERAND(ptr)
                  : [lane] "v"(lane * 16u), [mask] "v"(mask)
                  : TCSC_GATHER_CLOBBERS);
+#endif
 }
 
 // Scalar (SMEM) load of a chunk's header and its first TCSC_GEN_CAP entries.

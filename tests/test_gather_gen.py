@@ -29,6 +29,7 @@ RE_WAIT = re.compile(r"s_waitcnt lgkmcnt\((\d+)\)$")
 RE_IDX = re.compile(r"s_set_gpr_idx_(?:on|idx) s(\d+)")
 RE_FMA = re.compile(r"v_pk_fma_f32 v\[(\d+):\d+\], v\[(\d+):\d+\], s\[(\d+):\d+\], v\[(\d+):\d+\] op_sel_hi:\[1,0,1\]$")
 RE_CMP = re.compile(r"s_cmp_eq_u32 (s\d+), (\d+)$")
+RE_CMPLT = re.compile(r"s_cmp_lt_u32 (s\d+), (\d+)$")
 RE_SUB = re.compile(r"s_sub_u32 (s\d+), (s\d+), (\d+)$")
 RE_ADD = re.compile(r"s_add_u32 (s\d+), (s\d+), (\d+)$")
 RE_ADV = re.compile(r"s_add_u32 (s\d+), (s\d+), (s\d+)$")
@@ -68,6 +69,8 @@ def simulate(g, lines, nb, rem):
             continue
         if m := RE_CMP.match(ln):
             scc = regs[m[1]] == int(m[2])
+        elif m := RE_CMPLT.match(ln):
+            scc = regs[m[1]] < int(m[2])
         elif ln.startswith("s_cbranch_scc1 "):
             if scc:
                 pc = labels[ln.split()[1]]
@@ -119,11 +122,12 @@ GEOS = [dict(cw=16, batch=4, cap=24), dict(cw=16, batch=4, cap=16), dict(cw=16, 
         dict(cw=16, batch=2, cap=24)]
 
 
+@pytest.mark.parametrize("pf", [0, 3])
 @pytest.mark.parametrize("depth", [1, 2])
 @pytest.mark.parametrize("geo", GEOS, ids=lambda d: "b{batch}_c{cap}".format(**d))
-def test_tail_loop_gathers_each_entry_once(geo, depth):
+def test_tail_loop_gathers_each_entry_once(geo, depth, pf):
     try:
-        g = gen.Geo(budget=128, depth=depth, touch=0, tail=1, **geo)
+        g = gen.Geo(budget=128, depth=depth, touch=0, tail=1, pf=pf, **geo)
     except AssertionError as e:
         pytest.skip(f"geometry not valid at this depth: {e}")
     lines = gen.generate_tail(g)

@@ -54,12 +54,13 @@ import sys
 
 
 class Geo:
-    def __init__(self, cw, batch, cap, budget, depth=1, touch=4, tail=1, hdr=4):
+    def __init__(self, cw, batch, cap, budget, depth=1, touch=4, tail=1, hdr=4, pf=0):
         assert cw % 8 == 0 and cap % batch == 0 and 36 + hdr + 2 * cap <= 100
         assert hdr == 4 and (hdr + 2 * cap) % 4 == 0
         assert 1 <= depth and depth * batch <= 15, "lgkmcnt counts to 15"
         self.cw, self.batch, self.cap, self.budget, self.depth = cw, batch, cap, budget, depth
         self.touch = touch  # scalar-cache lines of the NEXT chunk's stream touched at the start
+        self.pf = pf  # scalar-cache lines of THIS stream past the buffer, touched when it will reload
         self.tail = bool(tail)
         self.npos = cap // batch
         assert self.npos > depth
@@ -204,6 +205,7 @@ def generate_tail(g):
         return []
     D = g.depth
     L = ["s_load_dword %[junk], %[tptr], " + hex(min(64 * t, 8 * g.cap - 4)) for t in range(g.touch)]
+    L += prefetch(g)
     L.append(".Lphase%=:")
     for p in range(g.npos):
         L += [f"s_cmp_eq_u32 {g.nb}, {p}", f"s_cbranch_scc1 .Ltail{p}%="]
@@ -230,7 +232,26 @@ def generate_tail(g):
             if not (p == g.npos - 1 and r == 0):
                 L.append("s_branch .Lend%=")
     L.append(".Lend%=:")
+    if g.pf:
+        L.append("s_waitcnt lgkmcnt(0)")  # a prefetch still in flight must land before %[junk] is released
     return L + advance(g)
+
+
+def prefetch(g):
+    """Streams longer than the buffer reload in place with an exposed scalar
+    load (cfg 2: ~38 entries per wave and chunk against 24).  When the header
+    says so (nb >= whole batches of a phase), touch the scalar-cache lines the
+    first reload will read, so it hits.  The touches land in %[junk]; while
+    they are in flight the counted LDS waits are conservative, never wrong."""
+    if not g.pf:
+        return []
+    first = 4 * g.hdr + 8 * g.cap  # bytes the buffer already holds
+    line0 = (first + 63) // 64 * 64
+    L = [f"s_cmp_lt_u32 {g.nb}, {g.npos}", "s_cbranch_scc1 .Lnopf%="]
+    L += [f"s_load_dword %[junk], s[{g.ptr}:{g.ptr + 1}], {hex(line0 + 64 * i)}" for i in range(g.pf)]
+    L.append(".Lnopf%=:")
+    return L
+
 
 def emit(f, name, lines):
     f.write(f"#define {name} \\\n")
@@ -271,6 +292,7 @@ def write_inc(path, g):
         else:
             f.write('#define TCSC_JUNK_OPERAND(j) [junk] "+s"(j)\n')
         f.write(f"#define TCSC_GEN_TOUCH {g.touch}\n")
+        f.write(f"#define TCSC_GEN_PF {g.pf}\n")
         clob = ['"memory"', '"scc"']
         clob += [f'"v{r}"' for r in range(g.xbase, g.xbase + g.nx)]
         f.write("#define TCSC_GATHER_CLOBBERS " + ", ".join(clob) + "\n")
@@ -294,11 +316,12 @@ def main():
     ap.add_argument("--touch", type=int, default=0)
     ap.add_argument("--tail", type=int, default=1)
     ap.add_argument("--hdr", type=int, default=4, help="chunk-header dwords ahead of the entries")
+    ap.add_argument("--pf", type=int, default=0, help="scalar-cache lines prefetched for a stream that will reload")
     here = os.path.dirname(os.path.abspath(__file__))
     ap.add_argument("-o", default=os.path.join(here, "..", "sparse-matrix-multiplication-benchmark_amd", "csrc",
                                                "gather_asm.inc"))
     a = ap.parse_args()
-    write_inc(a.o, Geo(a.cw, a.batch, a.cap, a.budget, a.depth, a.touch, a.tail, a.hdr))
+    write_inc(a.o, Geo(a.cw, a.batch, a.cap, a.budget, a.depth, a.touch, a.tail, a.hdr, a.pf))
     print(a.o)
 
 
