@@ -21,6 +21,6 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py ${BENCH_ARGS:-}
 if [ "${PROF:-1}" = 1 ]; then
   export TMPDIR=/tmp
-  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-api ${BENCH_ARGS:-}
+  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-api --no-graph ${BENCH_ARGS:-}
 fi
 echo ALL_DONE

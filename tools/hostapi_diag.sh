@@ -11,5 +11,5 @@ TCSC_HOST_BANDS=1 timeout -k 10 300 $B > gpurun_out/hb.json 2>/dev/null || exit 
 python -c "import json; d=json.load(open('gpurun_out/hb.json')); print('bench host_api unbanded', d['host_api']['ms'])"
 timeout -k 10 200 python tools/host_pipe_sweep.py 8 || exit 1
 rm -rf gpurun_out/prof
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-api > gpurun_out/rocprof.log 2>&1 || exit 1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-api --no-graph > gpurun_out/rocprof.log 2>&1 || exit 1
 echo rocprof ok
