@@ -11,6 +11,7 @@
 // unless TCSC_ON_ERROR=continue -- aborts, because silently leaving Y
 // unwritten would be worse than the reference's behaviour.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <hipblaslt/hipblaslt.h>
 #include <rocblas/rocblas.h>
 
@@ -1180,13 +1181,28 @@ class CopyPool {
     std::deque<std::function<void()>> q_;
 };
 
+// CPUs this process may run on (its affinity mask): the reference's
+// benchmark.sh runs the harness under `taskset -c 0` (benchmark.sh:36), and
+// copy workers confined to one core would be slower than the runtime's own
+// pageable copies.
+int usable_cpus() {
+    static const int n = [] {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        if (sched_getaffinity(0, sizeof set, &set) != 0) return 1;
+        return std::max(1, CPU_COUNT(&set));
+    }();
+    return n;
+}
+
 // Two pools, one per direction: with one shared FIFO a band's input copy
 // queues behind the previous band's output copy and the pipeline serialises.
+// Default: 8 workers each, fewer when the affinity mask holds fewer than 16 CPUs.
 CopyPool& copy_pool(int side) {
     static CopyPool* pools[2] = {nullptr, nullptr};
     static std::once_flag once;
     std::call_once(once, [] {
-        int n = 8;
+        int n = std::max(1, std::min(8, usable_cpus() / 2));
         if (const char* e = std::getenv("TCSC_HOST_THREADS")) n = std::max(1, std::min(64, std::atoi(e)));
         pools[0] = new CopyPool(n);
         pools[1] = new CopyPool(n);
@@ -1366,7 +1382,8 @@ struct Job {
 int host_bands(const tcsc_gpu_plan* p, int M, int K) {
     if (use_mfma(p, M) || use_small(p, M) || K <= 0) return 1;
     const double xbytes = (double)M * K * sizeof(float), MiB = 1024.0 * 1024;
-    int nb = xbytes < 48 * MiB ? 1 : std::max(4, std::min(8, (int)(xbytes / (8 * MiB))));
+    // the pipeline's copies need CPUs: none of it under `taskset -c 0` (benchmark.sh:36)
+    int nb = (xbytes < 48 * MiB || usable_cpus() < 4) ? 1 : std::max(4, std::min(8, (int)(xbytes / (8 * MiB))));
     if (const char* e = std::getenv("TCSC_HOST_BANDS")) nb = std::min(std::atoi(e), 64);
     nb = std::min(nb, M / tcsc::kTM);  // whole row tiles
     return nb < 2 ? 1 : nb;
