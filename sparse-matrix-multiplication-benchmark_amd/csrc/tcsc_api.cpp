@@ -1159,7 +1159,10 @@ class CopyPool {
                     if (--done->left == 0) done->cv.notify_all();
                 });
         }
-        cv_.notify_all();
+        if (parts.size() >= (size_t)n_)
+            cv_.notify_all();
+        else  // wake only as many workers as there are pieces
+            for (size_t i = 0; i < parts.size(); ++i) cv_.notify_one();
         return done;
     }
     static void wait(const Handle& done) {
@@ -1212,7 +1215,10 @@ CopyPool& copy_pool(int side) {
     std::call_once(once, [] {
         int n = std::max(1, std::min(8, usable_cpus() / 2));
         if (const char* e = std::getenv("TCSC_HOST_THREADS")) n = std::max(1, std::min(64, std::atoi(e)));
-        for (auto& p : pools) p = new CopyPool(n);
+        pools[0] = new CopyPool(n);
+        pools[1] = new CopyPool(n);
+        // the hash workers run while the copy pools mostly wait on PCIe: all usable CPUs, up to 16
+        pools[2] = new CopyPool(std::max(1, std::min(16, usable_cpus())));
     });
     return *pools[side];
 }
@@ -1232,7 +1238,9 @@ class AsyncFingerprint {
             return;
         }
         CopyPool& pool = copy_pool(2);
-        T_ = pool.size();
+        // ~256 K indices per piece: small arrays wake few workers
+        const long long total = (long long)W->n_elem_pos + W->n_elem_neg;
+        T_ = (int)std::max(1LL, std::min((long long)pool.size(), total >> 18));
         part_.assign(2 * T_, std::array<uint64_t, 4>{0, 0, 0, 0});
         std::vector<std::function<void()>> fs;
         const int* arr[2] = {W->row_index_pos, W->row_index_neg};
