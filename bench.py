@@ -8,20 +8,25 @@ A "step" is one pass of the hot path over one batch: one launch of the gfx950
 gather kernel computing Y = PReLU(X*W + b) for this rank's output columns,
 inputs already resident in HBM.  N=1 runs BASELINE configs[3] (cfg4: M=4096,
 K=N=16384, 98 % sparse, PReLU) -- the configuration the north star's target
-is quoted on.  With N ranks each GPU owns one column block:
-  --scaling weak   (default) every rank owns a full 16384-column block of a
-                   N*16384-column W (per-GPU work fixed as N grows);
-  --scaling strong the cfg4 matrix itself is split over the N ranks: into column
-                   blocks (--shard cols, X replicated) or row blocks (--shard rows:
-                   each rank stages only its rows of X; W is replicated).
+is quoted on.  With N ranks (the north star's "output-column
+shard across 8 x MI355X"):
+  --scaling strong (default) the cfg4 matrix itself is split over the N ranks:
+                   into column blocks (--shard cols, the default: X replicated,
+                   rank g owns columns [g*N/G, (g+1)*N/G)) or row blocks
+                   (--shard rows: each rank stages only its rows of X; W is
+                   replicated).  At N>1 the line also carries `alt_shard`, the
+                   other axis timed with the same protocol;
+  --scaling weak   every rank owns a full 16384-column block of a
+                   N*16384-column W (per-GPU work fixed as N grows).
 There is no collective on the data path; the only collectives are the
 timing barrier and the max-over-ranks of the elapsed time.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
 `roofline` for the gather kernel (algorithmic bytes per launch / average
 launch time measured with HIP events on the launch stream) and
-`cpu_baseline` (the oracle's restatement of tcsc_sgemm_prelu_basic timed on
-this host's cores on a bounded sample of the same workload).
+`cpu_baseline` (the reference's own sparse/tcsc.c, compiled in place into
+oracle/_ref, timed on this host's cores on a bounded sample of the same
+workload; its OpenMP form on every usable core beside it).
 """
 from __future__ import annotations
 
@@ -48,10 +53,13 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", type=int, default=4)
-    p.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    p.add_argument("--scaling", choices=("weak", "strong"), default="strong",
+                   help="strong (default): cfg's matrix split over the N ranks (--shard); weak: every rank a full copy")
     p.add_argument("--variant", default=None, help="override the config's variant")
     p.add_argument("--shard", choices=("cols", "rows"), default="cols",
                    help="strong scaling / --shard-of: split N (X replicated) or M (X split, W replicated)")
+    p.add_argument("--no-alt-shard", action="store_true",
+                   help="N>1 strong: skip the extra timing of the other split axis (rows when --shard cols)")
     p.add_argument("--shard-of", type=int, default=0,
                    help="time only rank 0's block of an S-way strong split (per-GPU view of S GPUs)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -205,6 +213,13 @@ def main():
     plan.prepare_x(X, cfg.M, sh)
     gather_s = timed(lambda: plan.sgemm_prepared(B, Y, cfg.M, ncols, variant, 0.2, sh), nsplit)
 
+    alt = None
+    if distributed and args.scaling == "strong" and not args.no_alt_shard and args.shard_of <= 1:
+        # the other collective-free split of the same config, timed with the same
+        # protocol (SURVEY.md §8e "Alternative"): row blocks when the line is column
+        # blocks.  Every rank takes part; rank 0 reports it beside the main line.
+        alt = alt_shard_line(args, tcsc_amd, workloads, cfg_full, variant, rank, world, dev, sh, stream)
+
     ops_rank = workloads.add_ops(cfg.M, nnz, ncols) * args.steps
     stats = torch.tensor([elapsed, float(ops_rank)], dtype=torch.float64,
                          device=dev if args.dist_backend == "nccl" else "cpu")
@@ -272,6 +287,8 @@ def main():
         }
         if validation is not None:
             out["validation"] = validation
+        if alt is not None:
+            out["alt_shard"] = alt
         if Wd is not None and not args.no_dense_baseline:
             # the reference's "TCSC vs Dense" line (main.cpp:379-391) on the
             # device -- gemm_basic's dense product with the same ternary W as an fp32 rocBLAS
@@ -328,6 +345,64 @@ def main():
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def alt_shard_line(args, tcsc_amd, workloads, cfg, variant, rank, world, dev, sh, stream):
+    """The strong-scaling split along the other axis (rows if the line splits
+    columns): warm-up, barrier + sync, `steps` steps, barrier + sync, max over
+    ranks; whole-job add-ops / that time.  Each rank holds the plan of the
+    whole W and its M/N rows of X (no collective on the data path)."""
+    import dataclasses
+
+    import torch
+    import torch.distributed as dist
+    from tcsc_amd.shard import column_range
+
+    shard = "rows" if args.shard == "cols" else "cols"
+    r0, r1, c0, c1 = 0, cfg.M, 0, cfg.N
+    if shard == "rows":
+        r0, r1 = column_range(cfg.M, world, rank)
+    else:
+        c0, c1 = column_range(cfg.N, world, rank)
+    ncols = c1 - c0
+    inp = workloads.make_device_inputs(cfg, c0, c1, dev)
+    csp = torch.empty(ncols + 1, dtype=torch.int32, device=dev)
+    csn = torch.empty(ncols + 1, dtype=torch.int32, device=dev)
+    npos, nneg = tcsc_amd.gpu_from_dense(inp["Wd"], cfg.K, ncols, csp, csn, stream=sh)
+    rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
+    rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
+    tcsc_amd.gpu_from_dense(inp["Wd"], cfg.K, ncols, csp, csn, rip, rin, stream=sh)
+    del inp["Wd"]
+    c = dataclasses.replace(cfg, M=r1 - r0)
+    X = inp["X"][r0:r1].contiguous()
+    B = inp["B"]
+    plan = tcsc_amd.Plan.from_device(c.K, ncols, csp, csn, rip, rin, 0, ncols, dev.index or 0, sh)
+    plan.reserve(c.M)
+    Y = torch.empty((c.M, ncols), device=dev)
+    for _ in range(max(args.warmup, 5)):
+        plan.sgemm(X, B, Y, c.M, ncols, variant, 0.2, sh)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan.sgemm(X, B, Y, c.M, ncols, variant, 0.2, sh)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    ops = workloads.add_ops(c.M, npos + nneg, ncols) * args.steps
+    st = torch.tensor([el, float(ops)], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+    t_max, o_tot = st[:1].clone(), st[1:].clone()
+    dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    dist.all_reduce(o_tot, op=dist.ReduceOp.SUM)
+    plan.destroy()
+    del X, Y, csp, csn, rip, rin, inp
+    torch.cuda.empty_cache()
+    return {"shard": shard, "value": float(o_tot.item()) / float(t_max.item()) / 1e9, "unit": "G-add-ops/s",
+            "ms_per_step": float(t_max.item()) / args.steps * 1e3, "rows_per_gpu": c.M, "columns_per_gpu": ncols,
+            "note": "same protocol as the line; X rows split (W replicated)" if shard == "rows" else
+                    "same protocol as the line; W columns split (X replicated)"}
 
 
 def host_api_line(tcsc_amd, cfg, ncols, variant, X, B, Y, csp, csn, rip, rin, adds, calls=6):
@@ -511,66 +586,115 @@ def bcsr_line(cfg, Wd, X, B, Y, nnz, tcsc_s, timed, sh, n):
     return res
 
 
+def usable_cpus():
+    """(cores this process may use, what the host reports): the affinity
+    mask, capped by the cgroup CPU quota when one is set (a GPU box's share
+    of a larger host), and os.cpu_count() / nproc for the record."""
+    n_host = os.cpu_count() or 1
+    try:
+        n_aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n_aff = n_host
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        quota = None
+    return (min(n_aff, quota) if quota else n_aff), {"nproc": n_host, "affinity": n_aff, "cgroup_quota_cpus": quota}
+
+
 def cpu_baseline(args, cfg, variant, X, B, csp, csn, rip, rin):
-    """The reference's own tcsc_sgemm_* (sparse/tcsc.c compiled in place into
-    oracle/_ref, IEEE flags) on 1 core when that build is present, else the
-    oracle's C restatement of it; the restatement on 1 core as well; and the
-    OpenMP sparseGEMM_PReLU restatement on all cores.  Row blocks of the same
-    workload until ~cpu_seconds of CPU work are spent (split between the two
-    1-core legs)."""
+    """SURVEY.md §8d, on this GPU box's host, rank 0 at N=1, on row samples
+    of the same workload (all columns):
+      * value: the reference's own tcsc_sgemm_<variant> (sparse/tcsc.c
+        compiled in place with its authors' flags, -O3 -ffast-math, AVX2+FMA:
+        oracle/_ref/libtcsc_ref_fast.so) on 1 core, as benchmark.sh pins it
+        (benchmark.sh:36): 1 warm-up pass, then the median of 3 passes;
+      * the same sources built IEEE (-O2, no fast-math: the parity build) and
+        the oracle's C restatement, each 1 core, median of 3;
+      * the reference's own OpenMP sparseGEMM_PReLU (SparseGEMM.h:151-168,
+        the multi-core form it ships) on every usable core, median of 3 over
+        all M rows.
+    Falls back to the oracle restatement ("port") where oracle/_ref is absent."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
 
     import pyoracle
 
     o = pyoracle.load_oracle()
-    ref = pyoracle.load_reference()
+    ref_fast = pyoracle.load_reference(fast=True)
+    ref_ieee = pyoracle.load_reference()
     ncols = csp.numel() - 1
     W = pyoracle.TCSC(cfg.K, ncols, csp.cpu().numpy(), csn.cpu().numpy(), rip.cpu().numpy(), rin.cpu().numpy())
     Bh = B.cpu().numpy()
+    Xh = X.cpu().numpy()
     nnz = W.nnz
     var = variant if variant in pyoracle.VARIANTS else "prelu_basic"
 
-    def one_core(fn, rows_per_block, budget):
-        # 1 core, row blocks of the reference's loop (tcsc.c:143-165)
-        done, t0 = 0, time.perf_counter()
-        while done < cfg.M:
-            r1 = min(cfg.M, done + rows_per_block)
-            fn(var, X[done:r1].cpu().numpy(), W, Bh, 0.2)
-            done = r1
-            if time.perf_counter() - t0 > budget:
-                break
-        t = time.perf_counter() - t0
-        return done, t, (done * nnz + done * ncols) / t / 1e9
+    def rate(rows, t):
+        return (rows * nnz + rows * ncols) / t / 1e9
 
-    budget = args.cpu_seconds / (2 if ref else 1)
-    # Reference.sgemm copies W's arrays per call: blocks of 128 rows keep that under ~3 %
-    ref_leg = one_core(ref.sgemm, 128, budget) if ref else None
-    done, t1, v_port = one_core(o.sgemm, 16, budget)
-    v1 = ref_leg[2] if ref else v_port
-    # all host cores (OpenMP, SparseGEMM.h:151-168 order)
-    threads = min(os.cpu_count() or 1, 16)
-    rows = min(cfg.M, max(64, done * threads))
-    Xs = X[:rows].cpu().numpy()
-    t2 = time.perf_counter()
-    o.sparse_gemm_omp(Xs, W, Bh, prelu=True, a=0.2, threads=threads)
-    t2 = time.perf_counter() - t2
-    vomp = (rows * nnz + rows * ncols) / t2 / 1e9
+    def one_core(fn, seconds):
+        """1 warm-up pass on 8 rows sizes the sample so that one pass takes
+        about `seconds`; then the median of 3 timed passes over it."""
+        t0 = time.perf_counter()
+        fn(var, Xh[:8], W, Bh, 0.2)
+        per_row = (time.perf_counter() - t0) / 8
+        rows = int(min(cfg.M, max(8, seconds / max(per_row, 1e-9))))
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            fn(var, Xh[:rows], W, Bh, 0.2)
+            ts.append(time.perf_counter() - t0)
+        t = float(np.median(ts))
+        return {"rows": rows, "median_s": t, "value": rate(rows, t)}
+
+    budget = args.cpu_seconds
+    legs = {}
+    if ref_fast:
+        legs["reference_fast"] = one_core(ref_fast.sgemm, budget * 0.14)
+    if ref_ieee:
+        legs["reference_ieee"] = one_core(ref_ieee.sgemm, budget * 0.07)
+    legs["port"] = one_core(o.sgemm, budget * 0.07)
+    threads, cpu_info = usable_cpus()
+    omp_env = os.environ.get("OMP_NUM_THREADS")
+    if omp_env:
+        threads = min(threads, int(omp_env)) if omp_env.isdigit() else threads
+    omp_lib = ref_fast or ref_ieee
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        if omp_lib:
+            o.set_omp_threads(threads)
+            omp_lib.sparse_gemm(Xh, W, Bh, prelu=True, a=0.2)
+        else:
+            o.sparse_gemm_omp(Xh, W, Bh, prelu=True, a=0.2, threads=threads)
+        ts.append(time.perf_counter() - t0)
+    t_omp = float(np.median(ts))
+    main = legs.get("reference_fast") or legs.get("reference_ieee") or legs["port"]
+    kind = "reference" if (ref_fast or ref_ieee) else "port"
+    flags = ("g++ -O3 -ffast-math -mavx2 -mfma (the reference's build_and_run_m1.sh:77 flags, "
+             "-march=native pinned to AVX2+FMA)" if ref_fast else
+             "g++ -O2 -fno-fast-math -ffp-contract=off (IEEE parity build)" if ref_ieee else "gcc -O2")
     out = {
-        "value": v1,
+        "value": main["value"],
         "unit": "G-add-ops/s",
         "cores": 1,
-        "kind": "reference" if ref else "port",
-        "sample": (f"{cfg.name}: first {ref_leg[0]} of {cfg.M} rows x all {ncols} columns, {var} "
-                   f"(the reference's sparse/tcsc.c compiled in place, g++ -O2 IEEE: oracle/Makefile), "
-                   f"{ref_leg[1]:.1f} s") if ref else
-                  (f"{cfg.name}: first {done} of {cfg.M} rows x all {ncols} columns, {var} "
-                   f"(oracle/tcsc_oracle.c, gcc -O2), {t1:.1f} s"),
-        "port_value": v_port,
-        "port_sample": f"first {done} rows, oracle/tcsc_oracle.c restatement, {t1:.1f} s",
-        "omp_value": vomp,
+        "kind": kind,
+        "sample": (f"{cfg.name}: first {main['rows']} of {cfg.M} rows x all {ncols} columns, tcsc_sgemm_{var}, "
+                   f"{'sparse/tcsc.c compiled in place' if kind == 'reference' else 'oracle/tcsc_oracle.c'} "
+                   f"({flags}), 1 core, 1 warm-up + median of 3 passes ({main['median_s']:.2f} s each)"),
+        "flags": flags,
+        "legs": legs,
+        "omp_value": rate(cfg.M, t_omp),
         "omp_cores": threads,
-        "omp_sample": f"first {rows} rows, oracle_sparse_gemm_omp ({threads} threads), {t2:.1f} s",
+        "omp_kind": "reference sparseGEMM_PReLU (SparseGEMM.h:151-168, OpenMP)" if omp_lib else
+                    "oracle_sparse_gemm_omp restatement",
+        "omp_sample": f"all {cfg.M} rows x {ncols} columns, median of 3 ({t_omp:.2f} s each)",
+        "host_cpus": cpu_info,
     }
     return out
 

@@ -28,7 +28,9 @@
  * and cached on every GPU used (the cache entry dies in tcsc_free); X and B
  * are copied host->device per call and Y is copied back.  With more than one
  * GPU visible the output columns are split into contiguous blocks, one per
- * GPU, with no collective (the blocks are copied straight into Y).
+ * GPU, with no collective: every GPU receives X, and its block is copied
+ * straight into its columns of Y (TCSC_SHARD_AXIS=rows splits the rows of
+ * X and Y instead, each GPU holding a plan of the whole W).
  * HIP failures are reported on stderr and through tcsc_gpu_last_error()
  * (include/tcsc_gpu.h) and then abort the process unless
  * TCSC_ON_ERROR=continue is set.

@@ -192,6 +192,18 @@ void tcsc_gpu_cache_clear(void);
 int tcsc_gpu_num_shards(void);
 void tcsc_gpu_set_num_shards(int shards);
 
+/* Host-side self-test hooks (no GPU needed; tests/test_sanitizers.py runs
+ * them in AddressSanitizer / ThreadSanitizer builds of the host code):
+ *   tcsc_selftest_fingerprint: the host API's plan-cache fingerprint of W
+ *     summed on its worker pool (the path host_sgemm overlaps with a call)
+ *     against the same hash summed serially; returns 0 when they agree.
+ *   tcsc_selftest_copy2d: `rows` rows of `row_bytes` from src (pitch sp)
+ *     to dst (pitch dp) on device `dev`'s copy pool for direction `side`
+ *     (0 in, 1 out) -- the pinned-staging copies of the band pipeline. */
+int tcsc_selftest_fingerprint(const tcsc_t *W);
+int tcsc_selftest_copy2d(void *dst, size_t dp, const void *src, size_t sp,
+                         size_t row_bytes, size_t rows, int dev, int side);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,6 +23,10 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libtcsc_ref.so")
+# the same sources built with the reference's own optimisation flags
+# (build_and_run_m1.sh:77: -O3 -ffast-math, -march=native pinned to AVX2+FMA):
+# a timing baseline only, never a parity oracle (fast-math re-associates)
+REF_FAST_SO = os.path.join(HERE, "_ref", "libtcsc_ref_fast.so")
 
 VARIANTS = ("basic", "optimized", "prelu_basic", "prelu_separate", "prelu_onthego")
 # the five bcsr_sgemm_* of sparse/bcsr.h:16-39, in the variant-id order of include/bcsr_gpu.h
@@ -253,6 +257,11 @@ class Oracle:
     def omp_max_threads(self) -> int:
         return int(self.lib.oracle_omp_max_threads())
 
+    def set_omp_threads(self, n: int) -> None:
+        """omp_set_num_threads for this thread: libgomp is one shared library,
+        so it also sets the team size of the reference's own OpenMP loops."""
+        C.CDLL("libgomp.so.1").omp_set_num_threads(int(n))
+
     # -- BCSR (oracle/bcsr_oracle.c) -------------------------------------------
     def bcsr_from_dense(self, dense: np.ndarray, r: int, c: int) -> BCSR:
         """bcsr.c:19-139."""
@@ -407,10 +416,11 @@ def load_oracle() -> Oracle:
     return _ORACLE
 
 
-def load_reference() -> Reference | None:
-    if not os.path.exists(REF_SO):
+def load_reference(fast: bool = False) -> Reference | None:
+    path = REF_FAST_SO if fast else REF_SO
+    if not os.path.exists(path):
         return None
-    return Reference()
+    return Reference(path)
 
 
 def prelu(v: np.ndarray, a: float) -> np.ndarray:

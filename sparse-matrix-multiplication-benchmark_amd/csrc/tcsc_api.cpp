@@ -27,6 +27,7 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <limits>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -691,10 +692,23 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
     }
     // gather-path limits: X^T row tiles of 64 rows on the transpose grid's y
     // axis (<= 65536 blocks) and 32-bit per-lane DMA offsets within a chunk
-    // (kTK rows of ldxt floats): M <= 2^22 rows per launch
-    if (M > (1 << 22)) {
-        set_error("tcsc_gpu_sgemm: M=%d rows in one launch (at most %d; split the rows)", M, 1 << 22);
-        return TCSC_E_ARG;
+    // (kTK rows of ldxt floats): at most 2^22 rows per launch.  A whole call
+    // (stage 0) runs as launches of 2^22 rows (whole row tiles) on the same
+    // workspace; the reference accepts any int M (tcsc.c:69).  Each row is
+    // summed as by one launch (M > 2^22 always takes 1 K-slice).
+    constexpr int kMaxLaunchRows = 1 << 22;
+    if (M > kMaxLaunchRows) {
+        if (stage != 0) {
+            set_error("tcsc_gpu_sgemm: M=%d rows staged at once (at most %d; split the rows)", M, kMaxLaunchRows);
+            return TCSC_E_ARG;
+        }
+        for (int r0 = 0; r0 < M; r0 += kMaxLaunchRows) {
+            const int r = std::min(kMaxLaunchRows, M - r0);
+            const int rc = sgemm_ws(p, dX + (size_t)r0 * p->rows, dB, dY + (size_t)r0 * ldy, r, ldy, variant, a,
+                                    stream, ws, ws_bytes, 0, force_slices);
+            if (rc != TCSC_OK) return rc;
+        }
+        return TCSC_OK;
     }
     const size_t xtb = tcsc::xt_bytes(M, p->rows);
     if (p->rows > 0 && (!ws || ws_bytes < xtb)) {
@@ -1058,15 +1072,20 @@ struct Shard {
 };
 
 // How the host API spreads a call over the GPUs ($TCSC_SHARD_AXIS, read when
-// a tcsc_t is first cached).  rows (default): block s of S owns rows
-// [M*s/S, M*(s+1)/S) of X and Y and uses its device's plan of the whole W --
-// each device receives only its rows of X over PCIe.  cols: block s owns the
-// columns [N*s/S, N*(s+1)/S) of W, B and Y, and every device receives all
-// of X.  Either way no data moves between the GPUs.
+// a tcsc_t is first cached).  cols (default, the north star's layout,
+// SURVEY.md §8e): block s of S owns the columns [N*s/S, N*(s+1)/S) of W, B
+// and Y, every device receives all of X, and each block's Y lands in its
+// columns of the caller's Y (a pitched D2H copy: the host-side concat).
+// rows: block s owns rows [M*s/S, M*(s+1)/S) of X and Y and uses its
+// device's plan of the whole W -- each device receives only its rows of X,
+// so the PCIe traffic of X is 1/S of the column split's (the better choice
+// when X dominates the copies, e.g. cfg 4 through host pointers).  Either
+// way no data moves between the GPUs and every element is summed as by one
+// launch.
 enum { kAxisRows = 0, kAxisCols = 1 };
 int shard_axis() {
     const char* e = std::getenv("TCSC_SHARD_AXIS");
-    return (e && std::strcmp(e, "cols") == 0) ? kAxisCols : kAxisRows;
+    return (e && std::strcmp(e, "rows") == 0) ? kAxisRows : kAxisCols;
 }
 
 struct CacheEntry {
@@ -1078,7 +1097,7 @@ struct CacheEntry {
     const int *csp = nullptr, *csn = nullptr, *rip = nullptr, *rin = nullptr;
     uint64_t content = 0;
     int order = TCSC_ORDER_FAST;  // the summation order the shards' plans were built for
-    int axis = kAxisRows;         // shard_axis() when built
+    int axis = kAxisCols;         // shard_axis() when built
     int blocks = 1;               // S: row or column blocks per call
     std::vector<Shard> shards;    // cols: one per column block; rows: one per device used
 };
@@ -1204,23 +1223,34 @@ int usable_cpus() {
     return n;
 }
 
-// Two pools, one per direction: with one shared FIFO a band's input copy
-// queues behind the previous band's output copy and the pipeline serialises.
-// Default: 8 workers each, fewer when the affinity mask holds fewer than 16 CPUs.
-// A third pool sums the plan-cache fingerprint while the call already runs
-// (host_sgemm), so it never waits behind the pipeline's copies.
-CopyPool& copy_pool(int side) {
-    static CopyPool* pools[3] = {nullptr, nullptr, nullptr};
-    static std::once_flag once;
-    std::call_once(once, [] {
-        int n = std::max(1, std::min(8, usable_cpus() / 2));
-        if (const char* e = std::getenv("TCSC_HOST_THREADS")) n = std::max(1, std::min(64, std::atoi(e)));
-        pools[0] = new CopyPool(n);
-        pools[1] = new CopyPool(n);
+// Two pools per device, one per direction: with one shared FIFO a band's
+// input copy queues behind the previous band's output copy and the pipeline
+// serialises; with one pool for all devices, 8 concurrent device pipelines
+// (one host thread per GPU) would queue behind each other.  Each device's
+// pools get min(8, usable CPUs / (2 x visible devices)) workers, at least 1
+// ($TCSC_HOST_THREADS overrides the count).  A third, process-wide pool sums
+// the plan-cache fingerprint while the call already runs (host_sgemm), so it
+// never waits behind the pipeline's copies.
+
+CopyPool& copy_pool(int side, int dev = 0) {
+    static std::mutex mu;
+    static std::vector<std::array<CopyPool*, 2>> per_dev;
+    static CopyPool* hash_pool = nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (side == 2) {
         // the hash workers run while the copy pools mostly wait on PCIe: all usable CPUs, up to 16
-        pools[2] = new CopyPool(std::max(1, std::min(16, usable_cpus())));
-    });
-    return *pools[side];
+        if (!hash_pool) hash_pool = new CopyPool(std::max(1, std::min(16, usable_cpus())));
+        return *hash_pool;
+    }
+    if (dev < 0) dev = 0;
+    if ((int)per_dev.size() <= dev) per_dev.resize(dev + 1, {nullptr, nullptr});
+    if (!per_dev[dev][side]) {
+        const int ndev = std::max(1, device_count_raw());
+        int n = std::max(1, std::min(8, usable_cpus() / (2 * ndev)));
+        if (const char* e = std::getenv("TCSC_HOST_THREADS")) n = std::max(1, std::min(64, std::atoi(e)));
+        per_dev[dev][side] = new CopyPool(n);
+    }
+    return *per_dev[dev][side];
 }
 
 // tcsc_fingerprint (same value) with the row-index arrays' 8-int groups
@@ -1504,8 +1534,8 @@ int run_bands(int dev, DevState& ds, const Shard& sh, int m0, int M, int nb, con
     const auto T0 = std::chrono::steady_clock::now();
     auto now_ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count(); };
     std::vector<double> t_in0(nbands), t_in1(nbands), t_out0(nbands), t_out1(nbands), t_wy(nbands);
-    CopyPool& pool_in = copy_pool(0);
-    CopyPool& pool_out = copy_pool(1);
+    CopyPool& pool_in = copy_pool(0, dev);
+    CopyPool& pool_out = copy_pool(1, dev);
     auto band = [&](int b, int* r0, int* r1) {
         *r0 = b * bm;
         *r1 = std::min(M, *r0 + bm);
@@ -1723,6 +1753,12 @@ void host_sgemm(int variant, const float* X, const tcsc_t* W, const float* B, fl
     if (speculative && fp.get() != e->content) {  // W's arrays changed in place: stale plan
         rerun = true;
         if ((rc = get_entry_locked(W, fp.get(), &e)) == TCSC_OK) rc = run(e);
+        if (rc != TCSC_OK) {
+            // Y holds the stale plan's product (or part of the rerun's): never leave
+            // that behind under TCSC_ON_ERROR=continue -- quiet NaN everywhere
+            const float qnan = std::numeric_limits<float>::quiet_NaN();
+            for (size_t i = 0; i < (size_t)M * N; ++i) Y[i] = qnan;
+        }
     }
     if (trace)
         std::fprintf(stderr, "[tcsc_amd] host call: %.1f us (%s%s)\n", us(),
@@ -1931,6 +1967,25 @@ void tcsc_dense_gemm(const float* X, const float* W, const float* b, float* Y, i
 
 void tcsc_dense_gemm_prelu(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, float a) {
     host_dense(TCSC_VARIANT_PRELU_BASIC, X, W, b, Y, M, N, K, a);
+}
+
+}  // extern "C"
+
+// Self-test hooks (include/tcsc_gpu.h): the worker pools without a GPU.
+extern "C" {
+
+int tcsc_selftest_fingerprint(const tcsc_t* W) {
+    if (!W) return -1;
+    AsyncFingerprint fp(W);
+    return fp.get() == tcsc_fingerprint(W) ? 0 : 1;
+}
+
+int tcsc_selftest_copy2d(void* dst, size_t dp, const void* src, size_t sp, size_t row_bytes, size_t rows, int dev,
+                         int side) {
+    if ((!dst || !src) && rows && row_bytes) return -1;
+    if (side != 0 && side != 1) return -1;
+    copy_pool(side, dev).copy2d(static_cast<char*>(dst), dp, static_cast<const char*>(src), sp, row_bytes, rows);
+    return 0;
 }
 
 }  // extern "C"

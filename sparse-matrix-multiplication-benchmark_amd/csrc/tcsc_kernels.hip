@@ -12,9 +12,10 @@
 // Kernel K1 (k_stream) -- DESIGN.md has the derivation and the measured
 // primitive rates it rests on:
 //  * lanes = rows.  A workgroup owns kTM = 256 rows of X (4 per lane) and
-//    kWaves*kCW = 256 output columns; it walks K in chunks of kTK = 64 rows.
-//    Each chunk of X is staged in LDS transposed (one 1-KiB row per k,
-//    double-buffered), so one nonzero of W is ONE conflict-free ds_read_b128
+//    kWaves*kCW = 256 output columns; it walks K in chunks of kTK = 48 rows.
+//    Each chunk of X^T is DMA'd into LDS (one 1-KiB row per k, a ring of
+//    kNBuf = 3 buffers, two chunks in flight), so one nonzero of W is ONE
+//    conflict-free ds_read_b128
 //    that every lane issues at the same k, then two v_pk_fma_f32 with a +-1
 //    scalar (an exact add/subtract).  No multiplies of data, no MFMA: W is
 //    ternary and 98 % sparse at the headline size.

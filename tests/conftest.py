@@ -20,6 +20,18 @@ for p in (ROOT, PKG, os.path.join(ROOT, "oracle")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (MI355X); run with -m gpu")
     config.addinivalue_line("markers", "slow: full BASELINE-size cases")
+    config.addinivalue_line("markers", "config_parity: the BASELINE-config / golden-fixture parity checks; "
+                                       "collected first so that a -x stop elsewhere never hides a config")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    """Run every `config_parity` test before everything else (stable order
+    inside both groups): the driver runs `pytest -x`, and the per-config
+    parity verdict must not depend on an unrelated test further down."""
+    first = [it for it in items if it.get_closest_marker("config_parity")]
+    if first:
+        rest = [it for it in items if not it.get_closest_marker("config_parity")]
+        items[:] = first + rest
 
 
 def load_golden(name):

@@ -36,8 +36,23 @@ def _run(extra):
     return lines[0]
 
 
-def test_two_ranks_weak_scaling():
+def test_two_ranks_default_is_cfg_column_split():
+    """The N>1 default is the north star's layout: the config itself (here
+    cfg 2) split over the ranks by output columns (strong scaling), plus the
+    row split of the same config as `alt_shard`."""
     d = _run([])
+    cfg = d["config"]
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert cfg["columns_per_gpu"] == 2048 and cfg["rows_per_gpu"] == 1024 and cfg["N"] == 4096
+    assert "column-shard x2 (strong)" in cfg["parallelism"]
+    alt = d["alt_shard"]
+    assert alt["shard"] == "rows" and alt["rows_per_gpu"] == 512 and alt["columns_per_gpu"] == 4096
+    assert alt["value"] > 0
+    assert d["validation"]["worst_err_over_bound"] <= 1.0
+
+
+def test_two_ranks_weak_scaling():
+    d = _run(["--scaling", "weak"])
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["steps"] == 3
     cfg = d["config"]
     per_rank = 1024 * cfg["nnz_per_gpu"] + 1024 * 4096  # add-ops of rank 0's block per step

@@ -200,6 +200,7 @@ def test_repeated_rows_in_a_column(gpu, oracle, path):
     W.free()
 
 
+@pytest.mark.config_parity
 def test_baseline_cfg5_sampled_rows(gpu, oracle, path):
     """BASELINE cfg 5 (M=2048, K=N=8192, 50 %) through the device API takes
     the MFMA path; sampled rows against the exact fp64 sums."""

@@ -63,6 +63,7 @@ def check_variant(g, variant, Y, oracle):
     assert ok, f"{variant}: worst err/bound = {ratio:.3g}"
 
 
+@pytest.mark.config_parity
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
 def test_host_api_all_variants(gpu, oracle, name):
     g = load_golden(name)
@@ -162,8 +163,8 @@ def test_prepare_then_gather_equals_sgemm(gpu, torch_cuda, name):
 @pytest.mark.parametrize("shards", [2, 3, 5])
 def test_multi_shard_host_path_equals_single(gpu, shards, axis, monkeypatch):
     """The host API's blocks (one per GPU on a node; several per device here)
-    concatenate to the single-block result bit for bit: row blocks
-    (TCSC_SHARD_AXIS=rows, the default) and column blocks."""
+    concatenate to the single-block result bit for bit: column blocks
+    (TCSC_SHARD_AXIS=cols, the default) and row blocks."""
     monkeypatch.setenv("TCSC_SHARD_AXIS", axis)
     g = load_golden("grid_m16_k512_n1024_nz8")
     W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
@@ -314,6 +315,7 @@ def run_device_cfg(torch, cfg, variant, x=None):
     return inp, W, Y, plan
 
 
+@pytest.mark.config_parity
 @pytest.mark.parametrize("cfg_idx", [2, 3, 4, 5])
 def test_baseline_config_sampled_rows(gpu, torch_cuda, oracle, cfg_idx):
     torch = torch_cuda

@@ -46,6 +46,7 @@ def assert_bits(Y, ref, what):
     np.testing.assert_array_equal(Y[~nan].view(np.uint32), ref[~nan].view(np.uint32), err_msg=what)
 
 
+@pytest.mark.config_parity
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
 def test_host_api_bit_exact_all_variants(reference_order, name):
     g = load_golden(name)
@@ -83,6 +84,7 @@ def test_plan_reports_its_order_and_switching_back(reference_order):
     W.free()
 
 
+@pytest.mark.config_parity
 @pytest.mark.parametrize("cfg_idx", [2, 3, 4])
 def test_baseline_sizes_sampled_rows_bit_exact(reference_order, oracle, cfg_idx):
     """Full BASELINE shapes through the device API (plan from device arrays,

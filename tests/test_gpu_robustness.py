@@ -251,3 +251,46 @@ def test_x_beyond_2_31_elements(gpu, torch_cuda, oracle, variant):
     Y64, S64 = oracle.f64_rows(Xs, W, B.cpu().numpy())
     ok, worst = pyoracle.check_close(Ys, Y64, S64, 0.2 if variant.startswith("prelu") else None)
     assert ok, worst
+
+
+def test_failed_rebuild_after_in_place_edit_poisons_y(gpu, oracle, monkeypatch):
+    """the host API runs a cached plan speculatively while the
+    fingerprint is summed.  If the arrays changed in place AND the rebuild
+    fails (here a row index moved outside [0, K)), the call must not return
+    the stale plan's product under TCSC_ON_ERROR=continue: Y is all NaN and
+    the error is reported."""
+    monkeypatch.setenv("TCSC_ON_ERROR", "continue")
+    M, K, N = 40, 120, 30
+    W = oracle.tcsc_from_dense(oracle.ternary((K, N), 0.1, 81))
+    Wl = to_lib(W)
+    Xi = oracle.integers((M, K), 82)
+    Bi = oracle.integers((N,), 83)
+    np.testing.assert_array_equal(tcsc_amd.sgemm("basic", Xi, Wl, Bi), oracle.sgemm("basic", Xi, W, Bi))
+    rip = Wl.row_index("pos")
+    rip[0] = K + 5  # in place, out of range: the plan rebuild refuses it
+    Y = np.zeros((M, N), np.float32)
+    tcsc_amd.sgemm("basic", Xi, Wl, Bi, Y=Y)
+    assert np.all(np.isnan(Y))
+    assert "row" in tcsc_amd.last_error().lower() or "index" in tcsc_amd.last_error().lower()
+    rip[0] = W.row_index_pos[0]  # repaired in place: a fresh plan, the right product again
+    np.testing.assert_array_equal(tcsc_amd.sgemm("basic", Xi, Wl, Bi), oracle.sgemm("basic", Xi, W, Bi))
+    Wl.free()
+
+
+def test_more_than_2pow22_rows_in_one_host_call(gpu, oracle, monkeypatch):
+    """the gather launches at most 2^22 rows; a host call with more
+    (unbanded, TCSC_HOST_BANDS=1) runs as several launches.  Integer inputs:
+    every sampled row bit-identical to the oracle, ragged last launch too."""
+    monkeypatch.setenv("TCSC_HOST_BANDS", "1")
+    M, K, N = (1 << 22) + 300, 16, 24
+    Wd = oracle.ternary((K, N), 0.15, 91)  # below the MFMA path's density: the gather
+    W = oracle.tcsc_from_dense(Wd)
+    Wl = tcsc_amd.TcscMatrix.from_dense(Wd)
+    rng = np.random.default_rng(92)
+    Xi = rng.integers(-512, 513, (M, K)).astype(np.float32)
+    Bi = rng.integers(-512, 513, N).astype(np.float32)
+    Y = tcsc_amd.sgemm("prelu_basic", Xi, Wl, Bi, 0.25)
+    rows = np.unique(np.concatenate([[0, (1 << 22) - 1, 1 << 22, M - 1], rng.integers(0, M, 60)]))
+    ref = oracle.sgemm("prelu_basic", Xi[rows], W, Bi, 0.25)
+    np.testing.assert_array_equal(Y[rows], ref)
+    Wl.free()
