@@ -18,7 +18,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <thread>
 #include <vector>
+#include <sched.h>
 
 #include "../../include/dense/dense.h"
 #include "../../include/sparse/tcsc.h"
@@ -257,13 +260,57 @@ bool compare(const dense_t result, const dense_t target, int rows, int cols) {
     return true;
 }
 
-void gemm_basic(const dense_t X, const dense_t W, const dense_t B, dense_t Y, int M, int N, int K) {
-    for (int m = 0; m < M; ++m)
-        for (int n = 0; n < N; ++n) {
-            float y = 0.0f;
-            for (int k = 0; k < K; ++k) y += X[(size_t)m * K + k] * W[(size_t)k * N + n];
-            Y[(size_t)m * N + n] = y + B[n];
+// The harness's dense oracle (dense.c:64-77): Y[m,n] = (sum_k X[m,k]*W[k,n])
+// + B[n], every element summed from 0 in ascending k with a rounded product
+// and a rounded add (no contraction), so the bits equal the reference's IEEE
+// build.  Loop order m, k, n (a row of accumulators) instead of m, n, k:
+// each element still sees the same sequence of operations, but W is read
+// along its rows, and row blocks run on the usable CPUs (the reference's
+// harness calls it >= 1,000 times per case at M = 256, main.cpp:376).
+namespace {
+void gemm_rows(const float* X, const float* W, const float* B, float* Y, int m0, int m1, int N, int K) {
+#pragma clang fp contract(off)
+    constexpr int R = 8;  // rows per pass over W: W is streamed M/R times instead of M times
+    std::vector<float> acc((size_t)R * N);
+    for (int mb = m0; mb < m1; mb += R) {
+        const int r = std::min(R, m1 - mb);
+        std::fill(acc.begin(), acc.end(), 0.0f);
+        for (int k = 0; k < K; ++k) {
+            const float* w = W + (size_t)k * N;
+            for (int i = 0; i < r; ++i) {
+                const float xv = X[(size_t)(mb + i) * K + k];
+                float* a = acc.data() + (size_t)i * N;
+                for (int n = 0; n < N; ++n) a[n] = a[n] + xv * w[n];
+            }
         }
+        for (int i = 0; i < r; ++i) {
+            float* y = Y + (size_t)(mb + i) * N;
+            const float* a = acc.data() + (size_t)i * N;
+            for (int n = 0; n < N; ++n) y[n] = a[n] + B[n];
+        }
+    }
+}
+int gemm_threads(int M, int N, int K) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    int cpus = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : 1;
+    // a thread per >= 4 M multiply-adds of work, at most 16 and one per row
+    const double work = (double)M * N * K;
+    return std::max(1, std::min({cpus, 16, M, (int)(work / 4e6) + 1}));
+}
+}  // namespace
+
+void gemm_basic(const dense_t X, const dense_t W, const dense_t B, dense_t Y, int M, int N, int K) {
+    if (M <= 0 || N <= 0) return;
+    const int T = gemm_threads(M, N, K);
+    if (T == 1) {
+        gemm_rows(X, W, B, Y, 0, M, N, K);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back(gemm_rows, X, W, B, Y, (int)((long long)M * t / T), (int)((long long)M * (t + 1) / T), N, K);
+    for (auto& x : th) x.join();
 }
 
 void gemm_prelu_basic(const dense_t X, const dense_t W, const dense_t B, float a, dense_t Y, int M, int N, int K) {

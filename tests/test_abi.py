@@ -253,3 +253,28 @@ def test_hand_built_tcsc_round_trips_and_plan_build_validates_rows(built_lib, or
     with pytest.raises(tcsc_amd.TcscError, match="col_start_neg"):
         tcsc_amd.Plan(bad)
     bad.free()
+
+
+@pytest.mark.parametrize("M,K,N,threads", [(1, 512, 2048, "1"), (37, 300, 129, "1"), (256, 512, 700, "")])
+def test_gemm_basic_bit_identical_to_reference(built_lib, oracle, M, K, N, threads, monkeypatch):
+    """dense/dense.h gemm_basic -- the harness's dense oracle (dense.c:64-77),
+    a CPU function of the library -- against the reference's own gemm_basic
+    (compiled in place, IEEE): same bits, on the row-blocked threaded path
+    too (a row of accumulators, k ascending per element)."""
+    import pyoracle
+
+    ref = pyoracle.load_reference()
+    if ref is None:
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    X = oracle.uniform((M, K), 301 + M)
+    Wd = oracle.ternary((K, N), 0.5, 302 + M)
+    Wd[0, :3] = [0.5, -2.0, 3.0]  # gemm_basic multiplies whatever W holds
+    B = oracle.uniform((N,), 303 + M)
+    import ctypes as C
+
+    Y = np.empty((M, N), np.float32)
+    f = built_lib.gemm_basic
+    fp = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+    f.argtypes, f.restype = [fp, fp, fp, fp, C.c_int, C.c_int, C.c_int], None
+    f(X.reshape(-1), np.ascontiguousarray(Wd).reshape(-1), B, Y.reshape(-1), M, N, K)
+    np.testing.assert_array_equal(Y.view(np.uint32), ref.gemm_basic(X, Wd, B).view(np.uint32))

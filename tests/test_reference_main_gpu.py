@@ -9,14 +9,15 @@ it validates every tcsc_sgemm_* variant with its own compare() (abs tol 1e-4,
 dense.c:42-59) against its own CPU gemm_basic and exit(1)s on a mismatch
 (main.cpp:299-368), then times all six functions with its cycle counter.
 
-The test runs it as a child process and requires "[OK] All validation tests
-passed!" for all five cases, with no "[ERROR]" line and no early exit.  Case
-5's timing leg (main.cpp:376, the naive CPU gemm_basic at 256x1024x4096 under
-REP=50) takes minutes, so the child is stopped once case 5 has validated; the
-four complete timing tables before it are parsed (harness/out2csv.py) to
-check that every legacy line is there.  The output is kept in
-gpurun_out/main_amd_out.txt when that directory exists (profiles/ holds a
-committed copy per round).
+The test runs it to the end as a child process and requires "[OK] All
+validation tests passed!" for all five cases, no "[ERROR]" line, exit status
+0, "ALL BENCHMARKS COMPLETED" and, parsed by harness/out2csv.py, the six
+legacy timing lines of every case.  (Its dense GEMM is the library's
+gemm_basic, the harness's CPU oracle: bit-identical to the reference's,
+tests/test_abi.py, but row-blocked and threaded, so the harness's >= 1,000
+timed calls per function (main.cpp:54-113) finish in minutes.)  The output
+is streamed into gpurun_out/main_amd_out.txt as it arrives when that
+directory exists (profiles/ holds a committed copy per round).
 """
 import os
 import signal
@@ -44,6 +45,9 @@ def test_reference_main_cpp_validates_every_case():
 
     env = dict(os.environ)
     env.pop("TCSC_PATH", None)
+    live = None
+    if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
+        live = open(os.path.join(ROOT, "gpurun_out", "main_amd_out.txt"), "w", buffering=1)
     p = subprocess.Popen([BIN], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, bufsize=1,
                          cwd=ROOT, env=env, start_new_session=True)
     lines, oks, errors = [], 0, []
@@ -51,28 +55,30 @@ def test_reference_main_cpp_validates_every_case():
     try:
         for line in p.stdout:
             lines.append(line.rstrip("\n"))
+            if live:
+                live.write(line)
             if "[ERROR]" in line:
                 errors.append(line.strip())
             if OK in line:
                 oks += 1
-                print(f"main_amd: case {oks} validated at {time.time() - t0:.1f} s", flush=True)
-                if oks == len(CASES):
-                    break
-            if time.time() - t0 > 600:
+                if live:
+                    live.write(f"# case {oks} validated at {time.time() - t0:.1f} s\n")
+            if time.time() - t0 > 480:
                 break
+        p.wait(timeout=30)
     finally:
         if p.poll() is None:
             os.killpg(p.pid, signal.SIGKILL)
-        p.wait()
+            p.wait()
+        if live:
+            live.write(f"# rc={p.returncode} after {time.time() - t0:.1f} s\n")
+            live.close()
     out = "\n".join(lines) + "\n"
-    if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
-        with open(os.path.join(ROOT, "gpurun_out", "main_amd_out.txt"), "w") as f:
-            f.write(out)
     assert not errors, errors
     assert oks == len(CASES), f"{oks} of {len(CASES)} cases validated; rc={p.returncode}\n{out[-3000:]}"
-    # cases 1-4 ran their timing legs to the end: every legacy line, parseable
+    assert p.returncode == 0 and "ALL BENCHMARKS COMPLETED" in out, out[-3000:]
     algos, cases = out2csv.parse(lines)
     assert [(c["M"], c["K"], c["N"]) for c in cases] == CASES
-    for c in cases[:4]:
+    for c in cases:
         for name in ("GEMM", "TCSC_basic", "TCSC_opt", "TCSC_PReLU_basic", "TCSC_PReLU_sep", "TCSC_PReLU_otg"):
             assert name in c["algo"] and float(c["algo"][name][0]) > 0, (c["M"], c["K"], c["N"], name)
