@@ -20,6 +20,8 @@ is streamed into gpurun_out/main_amd_out.txt as it arrives when that
 directory exists (profiles/ holds a committed copy per round).
 """
 import os
+import pty
+import select
 import signal
 import subprocess
 import sys
@@ -48,28 +50,53 @@ def test_reference_main_cpp_validates_every_case():
     live = None
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
         live = open(os.path.join(ROOT, "gpurun_out", "main_amd_out.txt"), "w", buffering=1)
-    p = subprocess.Popen([BIN], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, bufsize=1,
-                         cwd=ROOT, env=env, start_new_session=True)
+    # on a pseudo-terminal, so the harness's stdout is line-buffered (a pipe
+    # would hold its lines back in 4-KiB blocks)
+    master, slave = pty.openpty()
+    p = subprocess.Popen([BIN], stdin=subprocess.DEVNULL, stdout=slave, stderr=slave, cwd=ROOT, env=env,
+                         start_new_session=True)
+    os.close(slave)
     lines, oks, errors = [], 0, []
     t0 = time.time()
-    try:
-        for line in p.stdout:
-            lines.append(line.rstrip("\n"))
+    buf = b""
+
+    def take(chunk):
+        nonlocal buf, oks
+        buf += chunk
+        while b"\n" in buf:
+            raw, buf = buf.split(b"\n", 1)
+            line = raw.decode("utf-8", "replace").rstrip("\r")
+            lines.append(line)
             if live:
-                live.write(line)
+                live.write(line + "\n")
             if "[ERROR]" in line:
                 errors.append(line.strip())
             if OK in line:
                 oks += 1
                 if live:
                     live.write(f"# case {oks} validated at {time.time() - t0:.1f} s\n")
-            if time.time() - t0 > 480:
+
+    try:
+        while time.time() - t0 < 480:
+            r, _, _ = select.select([master], [], [], 1.0)
+            if r:
+                try:
+                    chunk = os.read(master, 65536)
+                except OSError:  # EIO: the child closed the terminal
+                    break
+                if not chunk:
+                    break
+                take(chunk)
+            elif p.poll() is not None:
                 break
         p.wait(timeout=30)
     finally:
         if p.poll() is None:
             os.killpg(p.pid, signal.SIGKILL)
             p.wait()
+        os.close(master)
+        if buf:
+            take(b"\n")
         if live:
             live.write(f"# rc={p.returncode} after {time.time() - t0:.1f} s\n")
             live.close()
