@@ -50,14 +50,18 @@ def test_reference_main_cpp_validates_every_case():
     live = None
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
         live = open(os.path.join(ROOT, "gpurun_out", "main_amd_out.txt"), "w", buffering=1)
-    # on a pseudo-terminal, so the harness's stdout is line-buffered (a pipe
-    # would hold its lines back in 4-KiB blocks)
-    master, slave = pty.openpty()
+    # a pseudo-terminal would make the harness's stdout line-buffered, but a
+    # GPU box may have none: a pipe (its output arrives in 4-KiB blocks) plus
+    # a heartbeat line in the live log every 20 s
+    try:
+        master, slave = pty.openpty()
+    except OSError:
+        master, slave = os.pipe()
     p = subprocess.Popen([BIN], stdin=subprocess.DEVNULL, stdout=slave, stderr=slave, cwd=ROOT, env=env,
                          start_new_session=True)
     os.close(slave)
     lines, oks, errors = [], 0, []
-    t0 = time.time()
+    t0 = beat = time.time()
     buf = b""
 
     def take(chunk):
@@ -89,6 +93,9 @@ def test_reference_main_cpp_validates_every_case():
                 take(chunk)
             elif p.poll() is not None:
                 break
+            if live and time.time() - beat > 20:
+                beat = time.time()
+                live.write(f"# ... {beat - t0:.0f} s, {oks} cases validated so far\n")
         p.wait(timeout=30)
     finally:
         if p.poll() is None:
