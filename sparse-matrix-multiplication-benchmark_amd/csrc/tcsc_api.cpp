@@ -984,6 +984,22 @@ int tcsc_gpu_sgemm_prepared(const tcsc_gpu_plan* p, const float* dB, float* dY, 
     return sgemm_ws(p, nullptr, dB, dY, M, ldy, variant, a, stream, p ? p->ws : nullptr, p ? p->ws_bytes : 0, 2);
 }
 
+// The two calls (counts, then fill) share the tile offsets: the first call
+// keeps them per device, keyed by (matrix, shape), and a second call on the
+// same key fills from them instead of counting again (cfg 4: two reads of
+// the 1-GiB matrix in all instead of three).  The fill writes at most the
+// counted entries, so index arrays sized from the first call are never
+// overrun even if the matrix changed in between.
+struct DenseBuildScratch {
+    const float* key = nullptr;
+    int rows = -1, cols = -1;
+    bool counted = false;
+    DevBuf cp, cn, totp, totn, tmp;
+    size_t tile_cap = 0, col_cap = 0, tmp_cap = 0;
+};
+std::mutex g_build_mu;
+std::vector<DenseBuildScratch> g_build;
+
 int tcsc_gpu_from_dense(const float* d_dense, int rows, int cols, int* d_csp, int* d_csn, int* d_rip, int* d_rin,
                         int* n_pos, int* n_neg, void* stream) {
     if (!d_csp || !d_csn || !n_pos || !n_neg || rows < 0 || cols < 0 || (!d_dense && rows * (long long)cols)) {
@@ -991,28 +1007,54 @@ int tcsc_gpu_from_dense(const float* d_dense, int rows, int cols, int* d_csp, in
         return TCSC_E_ARG;
     }
     hipStream_t st = static_cast<hipStream_t>(stream);
-    DevBuf cntp, cntn, tmp;
-    HIP_TRY(cntp.alloc((size_t)(cols + 1) * sizeof(int)));
-    HIP_TRY(cntn.alloc((size_t)(cols + 1) * sizeof(int)));
-    HIP_TRY(hipMemsetAsync(cntp.p, 0, (size_t)(cols + 1) * sizeof(int), st));
-    HIP_TRY(hipMemsetAsync(cntn.p, 0, (size_t)(cols + 1) * sizeof(int), st));
-    if (cols > 0 && rows > 0)
-        HIP_TRY(tcsc::dense_to_tcsc_counts(d_dense, rows, cols, cntp.as<int>(), cntn.as<int>(), st));
-    size_t tb = 0;
-    HIP_TRY(tcsc::plan_scan_tmp_bytes(cols + 1, &tb));
-    HIP_TRY(tmp.alloc(tb));
-    HIP_TRY(tcsc::exclusive_scan_i32(cntp.as<int>(), d_csp, cols + 1, tmp.p, tb, st));
-    HIP_TRY(tcsc::exclusive_scan_i32(cntn.as<int>(), d_csn, cols + 1, tmp.p, tb, st));
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_build_mu);
+    if ((int)g_build.size() <= dev) g_build.resize(dev + 1);
+    DenseBuildScratch& sc = g_build[dev];
+    const int tr = tcsc::dense_tile_rows(rows), nt = rows > 0 ? (rows + tr - 1) / tr : 0;
+    const size_t tile_b = std::max<size_t>(1, (size_t)nt * cols) * sizeof(int);
+    const size_t col_b = (size_t)(cols + 1) * sizeof(int);
+    const bool reuse = sc.counted && sc.key == d_dense && sc.rows == rows && sc.cols == cols && d_rip && d_rin;
+    if (!reuse) {
+        auto grow = [](DevBuf& b, size_t& cap, size_t want) -> hipError_t {
+            if (cap >= want && b.p) return hipSuccess;
+            if (b.p) (void)hipFree(b.p);
+            b.p = nullptr;
+            cap = 0;
+            const hipError_t e = b.alloc(want);
+            if (e == hipSuccess) cap = want;
+            return e;
+        };
+        size_t tb = 0;
+        HIP_TRY(tcsc::plan_scan_tmp_bytes(cols + 1, &tb));
+        size_t c1 = sc.tile_cap, c2 = sc.col_cap;
+        HIP_TRY(grow(sc.cp, sc.tile_cap, tile_b));
+        HIP_TRY(grow(sc.cn, c1, tile_b));
+        HIP_TRY(grow(sc.totp, sc.col_cap, col_b));
+        HIP_TRY(grow(sc.totn, c2, col_b));
+        HIP_TRY(grow(sc.tmp, sc.tmp_cap, tb));
+        sc.counted = false;
+        HIP_TRY(tcsc::dense_to_tcsc_counts(d_dense, rows, cols, sc.cp.as<int>(), sc.cn.as<int>(), sc.totp.as<int>(),
+                                           sc.totn.as<int>(), st));
+        sc.key = d_dense;
+        sc.rows = rows;
+        sc.cols = cols;
+        sc.counted = true;
+    }
+    size_t tb = sc.tmp_cap;
+    HIP_TRY(tcsc::exclusive_scan_i32(sc.totp.as<int>(), d_csp, cols + 1, sc.tmp.p, tb, st));
+    HIP_TRY(tcsc::exclusive_scan_i32(sc.totn.as<int>(), d_csn, cols + 1, sc.tmp.p, tb, st));
     int tot[2];
     HIP_TRY(hipMemcpyAsync(&tot[0], d_csp + cols, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(&tot[1], d_csn + cols, sizeof(int), hipMemcpyDeviceToHost, st));
+    if (d_rip && d_rin && cols > 0 && rows > 0)
+        HIP_TRY(tcsc::dense_to_tcsc_fill(d_dense, rows, cols, d_csp, d_csn, sc.cp.as<int>(), sc.cn.as<int>(), d_rip,
+                                         d_rin, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (d_rip && d_rin) sc.counted = false;  // a fill ends the pair
     *n_pos = tot[0];
     *n_neg = tot[1];
-    if (d_rip && d_rin && cols > 0 && rows > 0) {
-        HIP_TRY(tcsc::dense_to_tcsc_fill(d_dense, rows, cols, d_csp, d_csn, d_rip, d_rin, st));
-        HIP_TRY(hipStreamSynchronize(st));
-    }
     return TCSC_OK;
 }
 

@@ -135,9 +135,15 @@ size_t workspace_bytes(int M, int ncols, int slices);
 size_t xt_bytes(int M, int K);
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st);
 // tcsc_from_dense on the device
-hipError_t dense_to_tcsc_counts(const float* D, int rows, int cols, int* cntp, int* cntn, hipStream_t st);
-hipError_t dense_to_tcsc_fill(const float* D, int rows, int cols, const int* csp, const int* csn, int* rip,
-                              int* rin, hipStream_t st);
+// tile counts cp/cn ([row tile][col], dense_tile_rows(rows) rows per tile)
+// turned into per-column tile offsets in place; column totals into totp/totn
+// (cols + 1 entries, the last 0)
+int dense_tile_rows(int rows);
+hipError_t dense_to_tcsc_counts(const float* D, int rows, int cols, int* cp, int* cn, int* totp, int* totn,
+                                hipStream_t st);
+// row indices from the tile offsets op/on and col_start csp/csn
+hipError_t dense_to_tcsc_fill(const float* D, int rows, int cols, const int* csp, const int* csn, const int* op,
+                              const int* on, int* rip, int* rin, hipStream_t st);
 // Y[m, n] = act(Y[m, n] + B[n]) in place (the dense baseline's epilogue)
 hipError_t launch_bias_act(float* Y, int M, int N, int ldy, const float* B, bool prelu, float a, hipStream_t st);
 hipError_t exclusive_scan_i32(const int* in, int* out, int n, void* tmp, size_t tmp_bytes, hipStream_t st);

@@ -772,31 +772,112 @@ __global__ void k_bias_act(float* __restrict__ Y, int M, int N, int ldy, const f
 }
 
 // ---------------------------------------------------------------------------
-// Device tcsc_from_dense (bit-exact with tcsc.c:6-66): per-column counts,
-// exclusive scans, then a fill that keeps rows ascending inside a column.
+// Device tcsc_from_dense (bit-exact with tcsc.c:6-66): the K x N matrix is cut
+// into tiles of `tr` rows; one thread per (row tile, column) -- a wave reads
+// 64 consecutive columns of a row, 256 B coalesced, 8 rows in flight --
+// counts its +1.0f / -1.0f entries (k_dense_tile_counts), a per-column pass
+// turns the tile counts into tile offsets and column totals
+// (k_dense_tile_scan), the totals are scanned into col_start, and the same
+// threads walk their tile again writing row indices from their offsets
+// (k_dense_tile_fill): within a column the tiles follow each other in row
+// order and each walks its rows ascending, so every column's rows ascend as
+// in the reference's fill (tcsc.c:48-60).  Only == 1.0f / == -1.0f count
+// (tcsc.c:14-17,54-58).  HBM-bound: the matrix is read once per pass.
 // ---------------------------------------------------------------------------
-__global__ void k_dense_col_counts(const float* __restrict__ D, int rows, int cols, int* __restrict__ cntp,
-                                   int* __restrict__ cntn) {
-    for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < cols; n += gridDim.x * blockDim.x) {
-        int p = 0, q = 0;
-        for (int i = 0; i < rows; ++i) {
-            const float v = D[(size_t)i * cols + n];
-            p += (v == 1.0f);
-            q += (v == -1.0f);
+__global__ void __launch_bounds__(256) k_dense_tile_counts(const float* __restrict__ D, int rows, int cols, int tr,
+                                                           int* __restrict__ cp, int* __restrict__ cn) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= cols) return;
+    const int tile = blockIdx.y;
+    const int r0 = tile * tr, r1 = min(rows, r0 + tr);
+    const float* d = D + (size_t)r0 * cols + col;
+    int p = 0, q = 0, r = r0;
+    for (; r + 8 <= r1; r += 8) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = __builtin_nontemporal_load(d + (size_t)(r - r0 + i) * cols);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            p += v[i] == 1.0f;
+            q += v[i] == -1.0f;
         }
-        cntp[n] = p;
-        cntn[n] = q;
     }
+    for (; r < r1; ++r) {
+        const float v = d[(size_t)(r - r0) * cols];
+        p += v == 1.0f;
+        q += v == -1.0f;
+    }
+    cp[(size_t)tile * cols + col] = p;
+    cn[(size_t)tile * cols + col] = q;
 }
 
-__global__ void k_dense_fill(const float* __restrict__ D, int rows, int cols, const int* __restrict__ csp,
-                             const int* __restrict__ csn, int* __restrict__ rip, int* __restrict__ rin) {
-    for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < cols; n += gridDim.x * blockDim.x) {
-        int p = csp[n], q = csn[n];
-        for (int i = 0; i < rows; ++i) {
-            const float v = D[(size_t)i * cols + n];
-            if (v == 1.0f) rip[p++] = i;
-            else if (v == -1.0f) rin[q++] = i;
+// In place: tile counts -> exclusive offsets inside the column; totals into
+// totp/totn[col] (their [cols] entry is 0, so an exclusive scan of cols+1
+// entries ends in the grand total).
+__global__ void k_dense_tile_scan(int* __restrict__ cp, int* __restrict__ cn, int ntiles, int cols,
+                                  int* __restrict__ totp, int* __restrict__ totn) {
+    const int col = blockIdx.x * blockDim.x + threadIdx.x;
+    if (col > cols) return;
+    if (col == cols) {
+        totp[cols] = 0;
+        totn[cols] = 0;
+        return;
+    }
+    int sp = 0, sn = 0;
+    for (int t = 0; t < ntiles; ++t) {
+        const size_t i = (size_t)t * cols + col;
+        const int a = cp[i], b = cn[i];
+        cp[i] = sp;
+        cn[i] = sn;
+        sp += a;
+        sn += b;
+    }
+    totp[col] = sp;
+    totn[col] = sn;
+}
+
+// Writes at most the tile's counted entries (offsets of the next tile, or the
+// column's end): the arrays the caller sized from the counts are never
+// overrun, whatever the matrix holds by now.
+__global__ void __launch_bounds__(256) k_dense_tile_fill(const float* __restrict__ D, int rows, int cols, int tr,
+                                                         int ntiles, const int* __restrict__ csp,
+                                                         const int* __restrict__ csn, const int* __restrict__ op,
+                                                         const int* __restrict__ on, int* __restrict__ rip,
+                                                         int* __restrict__ rin) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= cols) return;
+    const int tile = blockIdx.y;
+    const size_t i = (size_t)tile * cols + col;
+    int p = csp[col] + op[i], q = csn[col] + on[i];
+    const int pend = tile + 1 < ntiles ? csp[col] + op[i + cols] : csp[col + 1];
+    const int qend = tile + 1 < ntiles ? csn[col] + on[i + cols] : csn[col + 1];
+    if (p == pend && q == qend) return;
+    const int r0 = tile * tr, r1 = min(rows, r0 + tr);
+    const float* d = D + (size_t)r0 * cols + col;
+    int r = r0;
+    for (; r + 8 <= r1; r += 8) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(d + (size_t)(r - r0 + k) * cols);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (v[k] == 1.0f) {
+                if (p < pend) rip[p] = r + k;
+                ++p;
+            } else if (v[k] == -1.0f) {
+                if (q < qend) rin[q] = r + k;
+                ++q;
+            }
+        }
+    }
+    for (; r < r1; ++r) {
+        const float v = d[(size_t)(r - r0) * cols];
+        if (v == 1.0f) {
+            if (p < pend) rip[p] = r;
+            ++p;
+        } else if (v == -1.0f) {
+            if (q < qend) rin[q] = r;
+            ++q;
         }
     }
 }
@@ -972,14 +1053,33 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
     return g.prelu ? launch_t<false, true>(g, s, st) : launch_t<false, false>(g, s, st);
 }
 
-hipError_t dense_to_tcsc_counts(const float* D, int rows, int cols, int* cntp, int* cntn, hipStream_t st) {
-    hipLaunchKernelGGL(k_dense_col_counts, dim3(grid_for(cols, 256)), dim3(256), 0, st, D, rows, cols, cntp, cntn);
+int dense_tile_rows(int rows) {
+    // 256-row tiles; taller ones when the grid's y extent (65535) needs them
+    int tr = 256;
+    while ((rows + tr - 1) / tr > 65535) tr *= 2;
+    return tr;
+}
+
+hipError_t dense_to_tcsc_counts(const float* D, int rows, int cols, int* cp, int* cn, int* totp, int* totn,
+                                hipStream_t st) {
+    const int tr = dense_tile_rows(rows), nt = (rows + tr - 1) / tr;
+    if (rows > 0 && cols > 0) {
+        hipLaunchKernelGGL(k_dense_tile_counts, dim3((cols + 255) / 256, nt), dim3(256), 0, st, D, rows, cols, tr, cp,
+                           cn);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_dense_tile_scan, dim3(cols / 256 + 1), dim3(256), 0, st, cp, cn, rows > 0 ? nt : 0, cols,
+                       totp, totn);
     return hipGetLastError();
 }
 
-hipError_t dense_to_tcsc_fill(const float* D, int rows, int cols, const int* csp, const int* csn, int* rip, int* rin,
-                              hipStream_t st) {
-    hipLaunchKernelGGL(k_dense_fill, dim3(grid_for(cols, 256)), dim3(256), 0, st, D, rows, cols, csp, csn, rip, rin);
+hipError_t dense_to_tcsc_fill(const float* D, int rows, int cols, const int* csp, const int* csn, const int* op,
+                              const int* on, int* rip, int* rin, hipStream_t st) {
+    const int tr = dense_tile_rows(rows), nt = (rows + tr - 1) / tr;
+    if (rows <= 0 || cols <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_dense_tile_fill, dim3((cols + 255) / 256, nt), dim3(256), 0, st, D, rows, cols, tr, nt, csp,
+                       csn, op, on, rip, rin);
     return hipGetLastError();
 }
 

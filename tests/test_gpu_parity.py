@@ -405,3 +405,63 @@ def test_host_bands_with_blocks_bit_identical(gpu, oracle, axis, shards, bands, 
     Y64, S64 = oracle.f64_rows(X, oracle.tcsc_from_dense(Wd), B)
     assert pyoracle.check_close(Yh, Y64, S64, 0.2)[0]
     W.free()
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 1), (7, 300), (257, 513), (1000, 64), (17_000_000, 3)])
+def test_gpu_from_dense_tiles_bitexact(gpu, torch_cuda, oracle, rows, cols):
+    """The tiled device builder (row tiles of 256, taller past 65535 tiles)
+    against the reference restatement: ragged tiles, one row, very tall
+    matrices, non-ternary values (they count as 0, tcsc.c:14-17)."""
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(rows * 7 + cols)
+    u = torch.rand((rows, cols), generator=g, device=dev)
+    d = torch.zeros((rows, cols), device=dev)
+    d[u < 0.03] = 1.0
+    d[(u >= 0.03) & (u < 0.06)] = -1.0
+    d[(u >= 0.06) & (u < 0.07)] = 0.5
+    d[(u >= 0.07) & (u < 0.08)] = -1.0000001
+    csp = torch.empty(cols + 1, dtype=torch.int32, device=dev)
+    csn = torch.empty(cols + 1, dtype=torch.int32, device=dev)
+    npos, nneg = tcsc_amd.gpu_from_dense(d, rows, cols, csp, csn)
+    rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
+    rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
+    tcsc_amd.gpu_from_dense(d, rows, cols, csp, csn, rip, rin)
+    torch.cuda.synchronize()
+    dn = d.cpu().numpy()
+    if rows * cols <= 1 << 22:
+        ref = oracle.tcsc_from_dense(dn)
+        ref_arrays = ref.arrays()
+    else:  # too tall for the C restatement's int offsets in reasonable time: numpy, column by column
+        ref_arrays = []
+        for val in (1.0, -1.0):
+            starts, idx = [0], []
+            for c in range(cols):
+                r = np.nonzero(dn[:, c] == val)[0].astype(np.int32)
+                idx.append(r)
+                starts.append(starts[-1] + r.size)
+            ref_arrays.append((np.array(starts, np.int32), np.concatenate(idx)))
+        ref_arrays = (ref_arrays[0][0], ref_arrays[1][0], ref_arrays[0][1], ref_arrays[1][1])
+    got = (csp.cpu().numpy(), csn.cpu().numpy(), rip[:npos].cpu().numpy(), rin[:nneg].cpu().numpy())
+    for a, b in zip(got, ref_arrays):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_gpu_from_dense_fill_never_overruns(gpu, torch_cuda):
+    """A matrix changed between the two calls: the fill writes at most the
+    entries the first call counted (the caller's arrays are sized from it)."""
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    rows, cols = 600, 40
+    d = torch.zeros((rows, cols), device=dev)
+    d[::7, :] = 1.0
+    csp = torch.empty(cols + 1, dtype=torch.int32, device=dev)
+    csn = torch.empty(cols + 1, dtype=torch.int32, device=dev)
+    npos, nneg = tcsc_amd.gpu_from_dense(d, rows, cols, csp, csn)
+    d[:, :] = 1.0  # many more +1 now
+    guard = torch.full((npos + 4096,), -7, dtype=torch.int32, device=dev)
+    rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
+    tcsc_amd.gpu_from_dense(d, rows, cols, csp, csn, guard[:max(npos, 1)], rin)
+    torch.cuda.synchronize()
+    assert torch.all(guard[npos:] == -7)
