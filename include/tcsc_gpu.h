@@ -129,18 +129,22 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan *plan);
  *        `cols` are not touched
  *   act: PReLU(v) = (v < 0 ? a*v : v) for the PRELU variants, identity
  *        otherwise.
- *   M  : at most 2^22 rows per launch on the gather path (TCSC_E_ARG
- *        beyond; offsets are 64-bit, so M*K may exceed 2^31).
+ *   M  : any; the gather path runs more than 2^22 rows as several
+ *        launches (offsets are 64-bit, so M*K may exceed 2^31).
  * Asynchronous on `stream`; once the workspace covers M (see
  * tcsc_gpu_plan_reserve) no allocation and no synchronisation (safe to
  * capture in a hipGraph).
  * Near-dense W (density >= 0.2, see tcsc_gpu_plan_info.mfma_min_M): launches
  * with M >= mfma_min_M run the MFMA path -- X split exactly into three bf16
- * parts and one rocBLAS bf16 GEMM with fp32 accumulation against the plan's
- * bf16 image of W -- with the same accuracy bounds as the gather (DESIGN.md
- * §4).  rocBLAS may allocate on its first call on a device: make one launch
- * before capturing such a plan.  $TCSC_PATH=gather|mfma at plan creation
- * disables / forces the path. */
+ * parts (k_split3) and one bf16 GEMM with fp32 accumulation against the
+ * plan's bf16 image of W on the matrix cores (k_gemm3, the library's own
+ * gfx950 kernel, bias and PReLU fused in its store), then the exact fixup of
+ * rows holding non-finite or tiny values (k_fixup) -- with the same accuracy
+ * bounds as the gather.  It allocates nothing per launch and
+ * keeps no state between launches, so graph replays with new X are exact.
+ * $TCSC_PATH=gather|mfma at plan creation disables / forces the path.
+ * Thread safety: concurrent launches of ONE plan (on any streams) share its
+ * workspace and are not supported; different plans are independent. */
 int tcsc_gpu_sgemm(const tcsc_gpu_plan *plan, const float *dX, const float *dB,
                    float *dY, int M, int ldy, int variant, float a,
                    void *stream);

@@ -12,7 +12,6 @@
 // unwritten would be worse than the reference's behaviour.
 #include <hip/hip_runtime.h>
 #include <sched.h>
-#include <hipblaslt/hipblaslt.h>
 #include <rocblas/rocblas.h>
 
 #include <algorithm>
@@ -40,16 +39,6 @@
 #include "../../include/tcsc_gpu.h"
 #include "tcsc_internal.h"
 
-// One hipBLASLt GEMM of the MFMA path (a launch shape of one plan): the
-// matmul descriptor, the three layouts and the algorithm the heuristic chose.
-struct LtGemm {
-    int M = 0, ldy = 0, bias = 0;
-    hipblasLtMatmulDesc_t desc = nullptr;
-    hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
-    hipblasLtMatmulAlgo_t algo{};
-    bool ok = false;
-};
-
 struct tcsc_gpu_plan {
     int device = 0;
     int rows = 0, cols = 0, col_begin = 0;
@@ -72,18 +61,16 @@ struct tcsc_gpu_plan {
     tcsc_gpu_plan* chain_pos = nullptr;
     tcsc_gpu_plan* chain_neg = nullptr;
     // MFMA path for near-dense W (tcsc_mfma.hip): W^T with
-    // three bf16 copies per column (cols x 3*rows), and the column range's rebased CSC for the
-    // rows the bf16 split of X cannot carry.  Launches with M >= mfma_min_M
-    // take it; null when the plan is gather-only.
+    // three bf16 copies per column (cols x mfma_ldk(rows)), and the column
+    // range's rebased CSC for the rows the bf16 split of X cannot carry.
+    // Launches with M >= mfma_min_M take it; null when the plan is gather-only.
     uint16_t* w3 = nullptr;
     size_t mfma_bytes = 0;
-    int mfma_gen = 0;  // staging generation of the MFMA path's row flags
     // the column range's rebased CSC (fast-order plans): the small-M path
     // walks it, the MFMA path's fixup recomputes flagged rows from it
     int *ccp = nullptr, *ccn = nullptr, *crp = nullptr, *crn = nullptr;
     size_t csc_bytes = 0;
     int mfma_min_M = 0;
-    std::vector<LtGemm> lt;  // hipBLASLt setups per (M, ldy, bias epilogue), made on first use
 };
 
 namespace {
@@ -248,8 +235,8 @@ int path_mode() {  // 0 auto, 1 gather only, 2 mfma forced
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// workspace of one MFMA launch: X3 (M x 3K bf16) + M row flags + "any"
-size_t mfma_ws_bytes(int M, int K) { return align256((size_t)M * 3 * K * 2) + (size_t)(M + 1) * sizeof(int); }
+// workspace of one MFMA launch: X3 (M x mfma_ldk(K) bf16) + M row flags
+size_t mfma_ws_bytes(int M, int K) { return align256((size_t)M * tcsc::mfma_ldk(K) * 2) + (size_t)M * sizeof(int); }
 
 // Variants 0-4 are the tcsc_sgemm_* family (sparse/tcsc.h); 5 is
 // SparseGEMM.h's sparseGEMM<float> (bias last, no activation).  Bias first
@@ -271,81 +258,7 @@ rocblas_handle rocblas_for_device(int dev) {
     return h;
 }
 
-hipblasLtHandle_t lt_for_device(int dev) {
-    static std::mutex mu;
-    static std::unordered_map<int, hipblasLtHandle_t> handles;
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = handles.find(dev);
-    if (it != handles.end()) return it->second;
-    hipblasLtHandle_t h = nullptr;
-    if (hipblasLtCreate(&h) != HIPBLAS_STATUS_SUCCESS) return nullptr;
-    handles[dev] = h;
-    return h;
-}
-
-void free_lt(LtGemm& g) {
-    if (g.la) (void)hipblasLtMatrixLayoutDestroy(g.la);
-    if (g.lb) (void)hipblasLtMatrixLayoutDestroy(g.lb);
-    if (g.lc) (void)hipblasLtMatrixLayoutDestroy(g.lc);
-    if (g.desc) (void)hipblasLtMatmulDescDestroy(g.desc);
-    g = LtGemm{};
-}
-
-// The MFMA path's GEMM as hipBLASLt sees it: D (cols x M, ld ldy, f32) =
-// op_T(W3T) (3K x cols bf16, k contiguous) . X3^T (3K x M bf16), fp32
-// accumulation, optionally + bias (the BIAS epilogue: bias added after the
-// sum, as the gather's bias-last variants).  The first launch of a shape asks
-// the heuristic for its best workspace-free algorithm (tools/hblt_bench.cpp:
-// ~10 % faster than rocBLAS gemm_ex's pick at cfg 5, and the epilogue saves
-// the separate bias pass); ok = false sends the launch to rocBLAS.
-LtGemm* lt_gemm_for(tcsc_gpu_plan* p, int M, int ldy, bool bias) {
-    for (auto& g : p->lt)
-        if (g.M == M && g.ldy == ldy && g.bias == (int)bias) return &g;
-    const char* force = std::getenv("TCSC_MFMA_GEMM");  // "rocblas": A/B against rocBLAS gemm_ex
-    hipblasLtHandle_t h = (force && std::strcmp(force, "rocblas") == 0) ? nullptr : lt_for_device(p->device);
-    LtGemm g;
-    g.M = M;
-    g.ldy = ldy;
-    g.bias = bias;
-    const int KK = 3 * p->rows, N = p->cols;
-    const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
-    const hipblasLtEpilogue_t epi = bias ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT;
-    const hipDataType bt = HIP_R_32F;
-    const uint64_t no_ws = 0;
-    hipblasLtMatmulPreference_t pref = nullptr;
-    hipblasLtMatmulHeuristicResult_t res{};
-    int n = 0;
-    g.ok = h && hipblasLtMatmulDescCreate(&g.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) == HIPBLAS_STATUS_SUCCESS &&
-           hipblasLtMatmulDescSetAttribute(g.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof ta) == HIPBLAS_STATUS_SUCCESS &&
-           hipblasLtMatmulDescSetAttribute(g.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof tb) == HIPBLAS_STATUS_SUCCESS &&
-           hipblasLtMatmulDescSetAttribute(g.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof epi) == HIPBLAS_STATUS_SUCCESS &&
-           (!bias || hipblasLtMatmulDescSetAttribute(g.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof bt) ==
-                         HIPBLAS_STATUS_SUCCESS) &&
-           hipblasLtMatrixLayoutCreate(&g.la, HIP_R_16BF, KK, N, KK) == HIPBLAS_STATUS_SUCCESS &&
-           hipblasLtMatrixLayoutCreate(&g.lb, HIP_R_16BF, KK, M, KK) == HIPBLAS_STATUS_SUCCESS &&
-           hipblasLtMatrixLayoutCreate(&g.lc, HIP_R_32F, N, M, ldy) == HIPBLAS_STATUS_SUCCESS &&
-           hipblasLtMatmulPreferenceCreate(&pref) == HIPBLAS_STATUS_SUCCESS &&
-           hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &no_ws,
-                                                 sizeof no_ws) == HIPBLAS_STATUS_SUCCESS &&
-           hipblasLtMatmulAlgoGetHeuristic(h, g.desc, g.la, g.lb, g.lc, g.lc, pref, 1, &res, &n) ==
-               HIPBLAS_STATUS_SUCCESS &&
-           n > 0 && res.state == HIPBLAS_STATUS_SUCCESS;
-    if (pref) (void)hipblasLtMatmulPreferenceDestroy(pref);
-    if (g.ok) {
-        g.algo = res.algo;
-    } else {
-        free_lt(g);
-        g.M = M;
-        g.ldy = ldy;
-        g.bias = bias;
-    }
-    p->lt.push_back(g);
-    return &p->lt.back();
-}
-
 void free_mfma(tcsc_gpu_plan* p) {
-    for (auto& g : p->lt) free_lt(g);
-    p->lt.clear();
     if (p->w3) (void)hipFree(p->w3);
     p->w3 = nullptr;
     p->mfma_bytes = 0;
@@ -415,15 +328,17 @@ int maybe_build_mfma(tcsc_gpu_plan* p, const int* csp, const int* csn, const int
         (void)hipGetLastError();
         return TCSC_OK;  // no room for the image: gather only
     }
-    if (hipMalloc(&p->w3, 3 * n * sizeof(uint16_t)) != hipSuccess) {
+    const int ldk = tcsc::mfma_ldk(p->rows);
+    const size_t w3b = (size_t)p->cols * ldk * sizeof(uint16_t);
+    if (hipMalloc(&p->w3, w3b) != hipSuccess) {
         (void)hipGetLastError();
         free_mfma(p);
         return TCSC_OK;
     }
-    p->mfma_bytes = 3 * n * sizeof(uint16_t);
+    p->mfma_bytes = w3b;
     HIP_TRY(hipMemsetAsync(bad.p, 0, sizeof(int), st));
-    HIP_TRY(tcsc::mfma_build_w3(csp, csn, rip, rin, col_begin, p->rows, p->cols, wf.as<float>(), p->w3, p->n_pos,
-                                p->n_neg, bad.as<int>(), st));
+    HIP_TRY(tcsc::mfma_build_w3(csp, csn, rip, rin, col_begin, p->rows, p->cols, wf.as<float>(), p->w3, ldk,
+                                p->n_pos, p->n_neg, bad.as<int>(), st));
     int hbad = 0;
     HIP_TRY(hipMemcpyAsync(&hbad, bad.p, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -593,13 +508,12 @@ class DeviceGuard {
 }  // namespace
 
 namespace {
-// The MFMA path (stage 0: all; 1: split only; 2: GEMM + epilogue on the
-// staged X3).  Y = [h|m|l] . [W;W;W] is, column-major, Y^T (cols x M, ld
-// ldy) = op_T(W3T) (cols x 3K; W3T stored 3K-contiguous per column) .
-// X3^T (3K x M, ld 3K).
+// The MFMA path (stage 0: all; 1: split only; 2: GEMM + fixup on the staged
+// X3): k_split3 (X -> X3 + row flags), k_gemm3 (Y = act(X3 . W3T^T + B),
+// the bias and PReLU in its store), k_fixup (the flagged rows, exact).
 int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy, int variant,
                float a, void* stream, float* ws, size_t ws_bytes, int stage) {
-    const int K = p->rows, N = p->cols;
+    const int K = p->rows, N = p->cols, ldk = tcsc::mfma_ldk(K);
     const size_t need = mfma_ws_bytes(M, K);
     if (!ws || ws_bytes < need) {
         set_error("tcsc_gpu_sgemm: workspace of %zu bytes < %zu needed for M=%d", ws ? ws_bytes : (size_t)0, need, M);
@@ -607,56 +521,13 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
     }
     hipStream_t st = static_cast<hipStream_t>(stream);
     uint16_t* x3 = reinterpret_cast<uint16_t*>(ws);
-    int* flags = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + align256((size_t)M * 3 * K * 2));
-    int* any = flags + M;
-    tcsc_gpu_plan* mp = const_cast<tcsc_gpu_plan*>(p);
-    if (stage != 2) {
-        mp->mfma_gen = mp->mfma_gen == 0x7fffffff ? 1 : mp->mfma_gen + 1;
-        HIP_TRY(tcsc::mfma_split_x(dX, M, K, x3, flags, any, mp->mfma_gen, st));
-    }
+    int* flags = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + align256((size_t)M * ldk * 2));
+    if (stage != 2) HIP_TRY(tcsc::mfma_split_x(dX, M, K, x3, ldk, flags, st));
     if (stage == 1) return TCSC_OK;
-    const float one = 1.0f, zero = 0.0f;
     const bool prelu = is_prelu(variant);
-    // hipBLASLt, with the bias in its epilogue unless a PReLU pass follows anyway
-    LtGemm* g = lt_gemm_for(const_cast<tcsc_gpu_plan*>(p), M, ldy, !prelu);
-    bool bias_done = false;
-    if (g->ok) {
-        if (g->bias && hipblasLtMatmulDescSetAttribute(g->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &dB,
-                                                       sizeof dB) != HIPBLAS_STATUS_SUCCESS) {
-            set_error("tcsc_gpu_sgemm: hipBLASLt bias pointer");
-            return TCSC_E_HIP;
-        }
-        const hipblasStatus_t ls = hipblasLtMatmul(lt_for_device(p->device), g->desc, &one, p->w3, g->la, x3, g->lb,
-                                                   &zero, dY, g->lc, dY, g->lc, &g->algo, nullptr, 0, st);
-        if (ls != HIPBLAS_STATUS_SUCCESS) {
-            set_error("tcsc_gpu_sgemm: hipblasLtMatmul failed (%d)", (int)ls);
-            return TCSC_E_HIP;
-        }
-        bias_done = g->bias;
-    } else {
-        rocblas_handle h = rocblas_for_device(p->device);
-        if (!h || rocblas_set_stream(h, st) != rocblas_status_success) {
-            set_error("tcsc_gpu_sgemm: no rocBLAS handle");
-            return TCSC_E_HIP;
-        }
-        const rocblas_status rs =
-            rocblas_gemm_ex(h, rocblas_operation_transpose, rocblas_operation_none, N, M, 3 * K, &one, p->w3,
-                            rocblas_datatype_bf16_r, 3 * K, x3, rocblas_datatype_bf16_r, 3 * K, &zero, dY,
-                            rocblas_datatype_f32_r, ldy, dY, rocblas_datatype_f32_r, ldy, rocblas_datatype_f32_r,
-                            rocblas_gemm_algo_standard, 0, 0);
-        if (rs != rocblas_status_success) {
-            set_error("tcsc_gpu_sgemm: rocblas_gemm_ex failed (%s)", rocblas_status_to_string(rs));
-            return TCSC_E_HIP;
-        }
-    }
-    // bias (+ PReLU) and the flagged rows' exact values in one pass, or only
-    // the flagged rows when the GEMM's epilogue added the bias
-    if (!bias_done)
-        HIP_TRY(tcsc::mfma_epilogue_fix(x3, M, K, p->ccp, p->ccn, p->crp, p->crn, N, dB, dY, ldy,
-                                        variant == TCSC_VARIANT_BASIC, prelu, a, flags, any, mp->mfma_gen, st));
-    else
-        HIP_TRY(tcsc::mfma_fixup(x3, M, K, p->ccp, p->ccn, p->crp, p->crn, N, dB, dY, ldy,
-                                 variant == TCSC_VARIANT_BASIC, prelu, a, flags, any, mp->mfma_gen, st));
+    HIP_TRY(tcsc::mfma_gemm3(x3, p->w3, ldk, M, N, dB, dY, ldy, prelu, a, st));
+    HIP_TRY(tcsc::mfma_fixup(x3, M, K, ldk, p->ccp, p->ccn, p->crp, p->crn, N, dB, dY, ldy,
+                             variant == TCSC_VARIANT_BASIC, prelu, a, flags, st));
     return TCSC_OK;
 }
 

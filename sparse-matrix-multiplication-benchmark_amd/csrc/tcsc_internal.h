@@ -169,32 +169,32 @@ hipError_t csc_copy(const int* csp, const int* csn, const int* rip, const int* r
                     long long n_pos, long long n_neg, int* cp, int* cn, int* crp, int* crn, hipStream_t st);
 
 // ---- MFMA path for near-dense W (tcsc_mfma.hip) ------------
+// X3 / W3T rows are ldk = mfma_ldk(K) bf16 long: [h | m | l] (X3) or
+// [w | w | w] (W3T), zero-padded to a multiple of the GEMM's 64-deep k step.
+inline int mfma_ldk(int K) { return (3 * K + 63) / 64 * 64; }
 // Build: wf (ncols x rows fp32 scratch) <- the +1/-1 entries of columns
 // [col_begin, col_begin+ncols) (absolute offsets), transposed; w3 <- W^T
-// with three bf16 copies per row (ncols x 3*rows).  *bad = 1 if a weight is
+// with three bf16 copies per row (ncols x ldk).  *bad = 1 if a weight is
 // not exact in bf16.
 hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int rows,
-                         int ncols, float* wf, uint16_t* w3, long long n_pos, long long n_neg, int* bad,
+                         int ncols, float* wf, uint16_t* w3, int ldk, long long n_pos, long long n_neg, int* bad,
                          hipStream_t st);
-
 // ---- small-M path (tcsc_small.hip) ----------------------------
 // Y[m, j] = act(B[j] + sum_P X[m,k] - sum_Q X[m,k]) for m < M <= 16, one wave
 // per column over the CSC copy.
 hipError_t launch_small_m(const float* X, int M, int K, const int* cp, const int* cn, const int* crp, const int* crn,
                           int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
                           hipStream_t st);
-// X (M x K) -> x3 (M x 3K bf16, [h | m | l]); flags[m] = gen and *any (=
-// flags + M) = gen mark the rows the fixup recomputes (gen: new per staging).
-hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int* flags, int* any, int gen, hipStream_t st);
-// Y = act(Y + B) with the rows flagged with gen recomputed exactly (the
-// epilogue after a GEMM without the bias).
-hipError_t mfma_epilogue_fix(const uint16_t* x3, int M, int K, const int* cp, const int* cn, const int* crp,
-                             const int* crn, int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu,
-                             float a, const int* flags, const int* any, int gen, hipStream_t st);
-// Rewrites the rows flagged with gen in k_stream's fast order (no-op if *any != gen).
-hipError_t mfma_fixup(const uint16_t* x3, int M, int K, const int* cp, const int* cn, const int* crp, const int* crn,
-                      int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
-                      const int* flags, const int* any, int gen, hipStream_t st);
+// X (M x K) -> x3 (M x ldk bf16, [h | m | l | 0..]); flags[m] = 1 for the
+// rows the fixup recomputes, 0 otherwise (every row, every call).
+hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int* flags, hipStream_t st);
+// k_gemm3: Y = act(x3 . w3^T + B) on the matrix cores (bias after the sum).
+hipError_t mfma_gemm3(const uint16_t* x3, const uint16_t* w3, int ldk, int M, int N, const float* B, float* Y,
+                      int ldy, bool prelu, float a, hipStream_t st);
+// Rewrites the flagged rows in k_stream's fast order (no-op when none is).
+hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cp, const int* cn, const int* crp,
+                      const int* crn, int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu,
+                      float a, const int* flags, hipStream_t st);
 
 // Error channel shared by every entry point of the library (tcsc_api.cpp):
 // the message behind tcsc_gpu_last_error(), and the host API's policy

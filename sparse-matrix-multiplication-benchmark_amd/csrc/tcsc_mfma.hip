@@ -2,24 +2,29 @@
 //
 // At 50 % density (BASELINE cfg 5) the gather walks half of W: 33.5 M
 // nonzeros x 2048 rows at ~27 T adds/s = 2.5 ms, while the matrix cores
-// multiply the dense W at ~1.7 PFLOP/s in bf16.  The path keeps fp32
-// results without an fp32 MFMA (0.15 PFLOP/s): every x is split exactly into
-// three bf16 parts, x = h + m + l (truncations of x and of its remainders:
-// 8 + 8 + 8 significand bits), W is exact in bf16 (0, +-1, or small
-// integers for duplicate rows), so each product is exact and the GEMM
+// multiply the dense W far faster in bf16.  The path keeps fp32 results
+// without an fp32 MFMA (the fp32 matrix rate is the vector rate): every x is
+// split exactly into three bf16 parts, x = h + m + l (truncations of x and of
+// its remainders: 8 + 8 + 8 significand bits), W is exact in bf16 (0, +-1,
+// or small integers for duplicate rows), so each product is exact and the
+// GEMM
 //     Y = [h | m | l] . [W ; W ; W]           (M x 3K) . (3K x N)
-// (W stored transposed, N x 3K, so both operands run along k)
-// accumulates in fp32 on the matrix cores (rocBLAS gemm_ex bf16 -> f32).
-// Only the summation order differs from the gather's: the result is within
-// the fast-order bound, and bit-exact on integer-valued inputs.
+// (both operands stored k-contiguous, rows padded with zeros to a multiple of
+// the 64-deep k step: X3 is M x ldk, W3T is N x ldk) accumulates in fp32 on
+// the matrix cores -- k_gemm3, written here for gfx950: 256 x 256 tiles of 8
+// waves (v_mfma_f32_16x16x32_bf16), the k steps staged into a 2-deep LDS
+// ring by LDS-DMA with a conflict-free swizzle, bias (+ PReLU) fused into
+// the store.  Only the summation order differs from the gather's: the result
+// is within the fast-order bound, and bit-exact on integer-valued inputs.
 //
 // Rows the split cannot carry are recomputed by the gather order: a
 // non-finite x would make inf*0 = NaN in columns whose W is 0 there (the
 // reference never touches those products), and bf16 MFMA inputs below
 // 2^-126 may be flushed.  k_split3 flags every row holding a non-finite x
-// or a nonzero |x| < 2^-100; k_fixup rewrites those rows from the plan's
-// per-column CSC copy, +1 and -1 rows merged in ascending k (+1 first on a
-// tie), bias first for tcsc_sgemm_basic, then the PReLU -- the exact
+// or a nonzero |x| < 2^-100 (it writes every row's flag on every call, so a
+// captured graph replays correctly); k_fixup rewrites those rows from the
+// plan's per-column CSC copy, +1 and -1 rows merged in ascending k (+1 first
+// on a tie), bias first for tcsc_sgemm_basic, then the PReLU -- the exact
 // arithmetic of k_stream's fast order.
 #include <hip/hip_runtime.h>
 
@@ -61,48 +66,45 @@ __device__ inline bool split3(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
     return x != 0.0f && fabsf(x) < 0x1p-100f;
 }
 
-// X (M x K, pitch K) -> X3 (M x 3K bf16, pitch 3K): [h | m | l] per row.
-// flags[m] = gen (and *any = gen) for a row the fixup must recompute; gen
-// is new for every staging, so the flags need no clearing (a stale value
-// equal to gen could only make the fixup recompute a row exactly).
-__global__ void k_split3(const float* __restrict__ X, int M, int K, uint16_t* __restrict__ X3,
-                         int* __restrict__ flags, int* __restrict__ any, int gen) {
-    const int kq = (K + 3) / 4;
-    const long long total = (long long)M * kq;
+// X (M x K, pitch K) -> X3 (M x ldk bf16): [h | m | l | 0 ...] per row, one
+// workgroup per row; flags[row] = 1 when the fixup must recompute the row,
+// else 0 (written every call).
+__global__ void __launch_bounds__(256) k_split3(const float* __restrict__ X, int M, int K, uint16_t* __restrict__ X3,
+                                               int ldk, int* __restrict__ flags) {
+    const int row = blockIdx.x;
+    const float* src = X + (size_t)row * K;
+    uint16_t* dst = X3 + (size_t)row * ldk;
     const bool vec = (K & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
-    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-         i += (long long)gridDim.x * blockDim.x) {
-        const int row = (int)(i / kq), k0 = 4 * (int)(i % kq);
-        const float* src = X + (size_t)row * K + k0;
+    bool fix = false;
+    const int kq = (K + 3) / 4;
+    for (int q = threadIdx.x; q < kq; q += blockDim.x) {
+        const int k0 = 4 * q;
         float v[4];
         if (vec) {
-            const float4 q = *reinterpret_cast<const float4*>(src);
-            v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+            typedef float f4 __attribute__((ext_vector_type(4)));
+            const f4 w = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src + k0));
+            v[0] = w.x, v[1] = w.y, v[2] = w.z, v[3] = w.w;
         } else {
-            for (int j = 0; j < 4; ++j) v[j] = k0 + j < K ? src[j] : 0.0f;
+            for (int j = 0; j < 4; ++j) v[j] = k0 + j < K ? src[k0 + j] : 0.0f;
         }
         uint16_t h[4], m[4], l[4];
-        bool fix = false;
         for (int j = 0; j < 4; ++j) fix |= split3(v[j], h[j], m[j], l[j]);
-        uint16_t* dst = X3 + (size_t)row * 3 * K + k0;
         if (vec) {
-            // 8-byte stores: k0 is a multiple of 4 and K too, so all three are aligned
             typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
-            *reinterpret_cast<u16x4*>(dst) = u16x4{h[0], h[1], h[2], h[3]};
-            *reinterpret_cast<u16x4*>(dst + K) = u16x4{m[0], m[1], m[2], m[3]};
-            *reinterpret_cast<u16x4*>(dst + 2 * (size_t)K) = u16x4{l[0], l[1], l[2], l[3]};
+            *reinterpret_cast<u16x4*>(dst + k0) = u16x4{h[0], h[1], h[2], h[3]};
+            *reinterpret_cast<u16x4*>(dst + K + k0) = u16x4{m[0], m[1], m[2], m[3]};
+            *reinterpret_cast<u16x4*>(dst + 2 * K + k0) = u16x4{l[0], l[1], l[2], l[3]};
         } else {
             for (int j = 0; j < 4 && k0 + j < K; ++j) {
-                dst[j] = h[j];
-                dst[K + j] = m[j];
-                dst[2 * (size_t)K + j] = l[j];
+                dst[k0 + j] = h[j];
+                dst[K + k0 + j] = m[j];
+                dst[2 * K + k0 + j] = l[j];
             }
         }
-        if (fix) {
-            flags[row] = gen;
-            *any = gen;
-        }
     }
+    for (int k = 3 * K + threadIdx.x; k < ldk; k += blockDim.x) dst[k] = 0;
+    fix = __syncthreads_or(fix);
+    if (threadIdx.x == 0) flags[row] = fix ? 1 : 0;
 }
 
 // The +1/-1 entries of column j (rebased CSC) added into a dense fp32 image
@@ -118,11 +120,10 @@ __global__ void k_w_scatter(const int* __restrict__ cs, const int* __restrict__ 
     for (int e = e0 + lane; e < e1; e += 64) atomicAdd(&WfT[(size_t)j * K + r[e]], sign);
 }
 
-// WfT (ncols x K fp32) -> W3T (ncols x 3K bf16): row n = [w | w | w], so both
-// GEMM operands run along k (the "TN" form, ~8 % faster than W3 as 3K x
-// ncols: tools/dense3_bench.cpp).  Values must be integers of magnitude
-// <= 256 to be exact in bf16; *bad = 1 otherwise.
-__global__ void k_w3_from(const float* __restrict__ WfT, int ncols, int K, uint16_t* __restrict__ W3T,
+// WfT (ncols x K fp32) -> W3T (ncols x ldk bf16): row n = [w | w | w | 0..],
+// so both GEMM operands run along k (the pad was zeroed before).  Values must
+// be integers of magnitude <= 256 to be exact in bf16; *bad = 1 otherwise.
+__global__ void k_w3_from(const float* __restrict__ WfT, int ncols, int K, uint16_t* __restrict__ W3T, int ldk,
                           int* __restrict__ bad) {
     const long long n = (long long)ncols * K;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
@@ -131,7 +132,7 @@ __global__ void k_w3_from(const float* __restrict__ WfT, int ncols, int K, uint1
         if (fabsf(w) > 256.0f) *bad = 1;
         const uint16_t b = (uint16_t)(f2u(w) >> 16);
         const long long j = i / K, k = i - j * K;
-        uint16_t* row = W3T + j * 3 * K;
+        uint16_t* row = W3T + j * ldk;
         row[k] = b;
         row[K + k] = b;
         row[2 * K + k] = b;
@@ -151,11 +152,11 @@ __global__ void k_copy_from(const int* __restrict__ src, const int* __restrict__
 // comment): x rebuilt from its three parts, +1 and -1 rows merged in
 // ascending k, the bias first or last, then the PReLU.
 template <bool BIAS_FIRST, bool PRELU>
-__device__ inline float exact_out(const uint16_t* __restrict__ X3, int K, const int* __restrict__ cp,
+__device__ inline float exact_out(const uint16_t* __restrict__ X3, int K, int ldk, const int* __restrict__ cp,
                                   const int* __restrict__ cn, const int* __restrict__ rp,
                                   const int* __restrict__ rn, const float* __restrict__ Bias, int row, int j,
                                   float a) {
-    const uint16_t* x3 = X3 + (size_t)row * 3 * K;
+    const uint16_t* x3 = X3 + (size_t)row * ldk;
     auto xk = [&](int k) {
         return (u2f((uint32_t)x3[k] << 16) + u2f((uint32_t)x3[K + k] << 16)) + u2f((uint32_t)x3[2 * K + k] << 16);
     };
@@ -176,60 +177,152 @@ __device__ inline float exact_out(const uint16_t* __restrict__ X3, int K, const 
     return acc;
 }
 
-// Flagged rows, after a GEMM that already added the bias (no PReLU).  One
-// thread per column; every block walks the flag list.
+// Flagged rows, after the GEMM (which wrote act(sum + bias) for every row):
+// one thread per column.  A block first ORs the row flags; most calls have
+// none and the kernel ends there.
 template <bool BIAS_FIRST, bool PRELU>
-__global__ void k_fixup(const uint16_t* __restrict__ X3, int M, int K, const int* __restrict__ cp,
-                        const int* __restrict__ cn, const int* __restrict__ rp, const int* __restrict__ rn,
-                        int ncols, const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a,
-                        const int* __restrict__ flags, const int* __restrict__ any, int gen) {
-    if (*any != gen) return;
+__global__ void __launch_bounds__(256) k_fixup(const uint16_t* __restrict__ X3, int M, int K, int ldk,
+                                               const int* __restrict__ cp, const int* __restrict__ cn,
+                                               const int* __restrict__ rp, const int* __restrict__ rn, int ncols,
+                                               const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a,
+                                               const int* __restrict__ flags) {
+    int any = 0;
+    for (int r = threadIdx.x; r < M; r += blockDim.x) any |= flags[r];
+    if (!__syncthreads_or(any)) return;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= ncols) return;
     for (int row = 0; row < M; ++row)
-        if (flags[row] == gen)
-            Y[(size_t)row * ldy + j] = exact_out<BIAS_FIRST, PRELU>(X3, K, cp, cn, rp, rn, Bias, row, j, a);
+        if (flags[row])
+            Y[(size_t)row * ldy + j] = exact_out<BIAS_FIRST, PRELU>(X3, K, ldk, cp, cn, rp, rn, Bias, row, j, a);
 }
 
-// The epilogue after a plain GEMM, with the fixup folded in: Y = act(Y + B)
-// for the rows the split carried, the exact fast-order value for the
-// flagged ones.  One launch instead of two.
-template <bool BIAS_FIRST, bool PRELU>
-__global__ void k_epilogue_fix(float* __restrict__ Y, int M, int N, int ldy, const float* __restrict__ Bias, float a,
-                               const uint16_t* __restrict__ X3, int K, const int* __restrict__ cp,
-                               const int* __restrict__ cn, const int* __restrict__ rp, const int* __restrict__ rn,
-                               const int* __restrict__ flags, const int* __restrict__ any, int gen) {
-    const bool some = *any == gen;
-    const int nq = (N + 3) / 4;
-    const long long total = (long long)M * nq;
-    const bool vec = (ldy & 3) == 0 && (N & 3) == 0 && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0);
-    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-         i += (long long)gridDim.x * blockDim.x) {
-        const int m = (int)(i / nq), n = 4 * (int)(i % nq);
-        float* y = Y + (size_t)m * ldy + n;
-        if (some && flags[m] == gen) {
-            for (int c = 0; c < 4 && n + c < N; ++c)
-                y[c] = exact_out<BIAS_FIRST, PRELU>(X3, K, cp, cn, rp, rn, Bias, m, n + c, a);
-            continue;
-        }
-        if (vec) {
-            float4 v = *reinterpret_cast<float4*>(y);
-            v.x += Bias[n + 0];
-            v.y += Bias[n + 1];
-            v.z += Bias[n + 2];
-            v.w += Bias[n + 3];
-            if (PRELU) {
-                v.x = (v.x < 0.0f) ? a * v.x : v.x;
-                v.y = (v.y < 0.0f) ? a * v.y : v.y;
-                v.z = (v.z < 0.0f) ? a * v.z : v.z;
-                v.w = (v.w < 0.0f) ? a * v.w : v.w;
-            }
-            *reinterpret_cast<float4*>(y) = v;
+// ---------------------------------------------------------------------------
+// k_gemm3: Y[m, n] = act(sum_k A[m, k] * Bt[n, k] + bias[n]), bf16 in, fp32
+// accumulate, A = X3 (M x ldk), Bt = W3T (N x ldk), ldk % 64 == 0.
+//
+// * Tile TM x TN = (WM*FI*16) x (WN*FJ*16) per workgroup of WM*WN waves; a
+//   wave owns FI x FJ blocks of 16 x 16 (v_mfma_f32_16x16x32_bf16, 4 fp32
+//   accumulators per lane per block).  256 x 256 with 8 waves (2 x 4, 128 x
+//   64 per wave) for the large shapes; 128 x 128 with 4 waves for grids that
+//   would leave CUs idle.
+// * k steps of 64 staged in a 2-deep LDS ring by LDS-DMA
+//   (global_load_lds_dwordx4: 1 KiB per wave-instruction, no VGPRs): step
+//   t+1 is in flight while step t is multiplied; one vmcnt(0) + barrier per
+//   step.
+// * LDS image of a stage: A's rows, then B's, in 1-KiB pieces of 8 rows x 64
+//   k (128 B per row).  Inside a piece the 16-B granule g (8 k) of row r sits
+//   at slot 8r + (g ^ r): the DMA writes the piece lane-linear (lane = slot)
+//   from per-lane source addresses, and the MFMA fragment reads (lane l:
+//   row l & 15 of a 16-row block, granule 4*kh + l/16) then hit 16 distinct
+//   16-B slots in every ds_read_b128 lane group: conflict-free (4 LDS
+//   cycles per read instead of 16-32 for a linear image).
+// * Rows past M / N load the last valid row (in bounds) and are not stored.
+// * Tile order: XCD-aware and bijective; an XCD's ~32 concurrent workgroups
+//   take 8 row tiles x 4 column tiles, sharing A and B tiles in its L2.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int WM, int WN, int FI, int FJ, bool PRELU>
+__global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                                                      int ldk, int M, int N, int ksteps,
+                                                      const float* __restrict__ bias, float* __restrict__ Y, int ldy,
+                                                      float a, int tiles_m, int tiles_n) {
+    constexpr int TM = WM * FI * 16, TN = WN * FJ * 16, NW = WM * WN;
+    constexpr int PA = TM / 8, PB = TN / 8;  // 1-KiB pieces per stage
+    constexpr int STAGE = (PA + PB) * 1024;
+    constexpr int PPW = (PA + PB) / NW;      // pieces each wave moves per stage
+    static_assert((PA + PB) % NW == 0, "whole pieces per wave");
+    __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wave / WN, wc = wave % WN;
+
+    // XCD-aware bijective renumbering, then groups of tiles_m x 4 tiles
+    const int T = tiles_m * tiles_n, L = blockIdx.x;
+    const int q = T >> 3, r = T & 7, x = L & 7;
+    const int Lg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
+    const int grp = Lg / (tiles_m * 4), idx = Lg % (tiles_m * 4);
+    const int tm = idx % tiles_m, tn = grp * 4 + idx / tiles_m;
+    const int m0 = tm * TM, n0 = tn * TN;
+
+    // this wave's DMA pieces: per-lane sources (row clamped into the matrix)
+    const int row_in = lane >> 3, gsel = (lane & 7) ^ row_in;
+    const uint16_t* src[PPW];
+    int dst[PPW];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        const int piece = wave * PPW + i;
+        if (piece < PA) {
+            const int rr = min(m0 + 8 * piece + row_in, M - 1);
+            src[i] = A + (size_t)rr * ldk + 8 * gsel;
         } else {
-            for (int c = 0; c < 4 && n + c < N; ++c) {
-                float v = y[c] + Bias[n + c];
+            const int rr = min(n0 + 8 * (piece - PA) + row_in, N - 1);
+            src[i] = Bt + (size_t)rr * ldk + 8 * gsel;
+        }
+        dst[i] = piece * 1024;
+    }
+    auto dma = [&](int kstep, int buf) {
+#pragma unroll
+        for (int i = 0; i < PPW; ++i)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + (size_t)kstep * 64),
+                                             (__attribute__((address_space(3))) void*)(lds + buf * STAGE + dst[i]),
+                                             16, 0, 0);
+    };
+
+    // fragment read offsets inside a 16-row block (the swizzle above)
+    int foff[2];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+        foff[kh] = ((lane & 15) >> 3) * 1024 + 16 * (8 * (lane & 7) + ((4 * kh + (lane >> 4)) ^ (lane & 7)));
+
+    f32x4 acc[FI][FJ];
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    dma(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = 0; t < ksteps; ++t) {
+        const int buf = t & 1;
+        if (t + 1 < ksteps) dma(t + 1, buf ^ 1);
+        const char* sb = lds + buf * STAGE;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+            bf16x8 af[FI], bfr[FJ];
+#pragma unroll
+            for (int j = 0; j < FJ; ++j)
+                bfr[j] = *reinterpret_cast<const bf16x8*>(sb + (PA + (wc * FJ + j) * 2) * 1024 + foff[kh]);
+#pragma unroll
+            for (int i = 0; i < FI; ++i)
+                af[i] = *reinterpret_cast<const bf16x8*>(sb + ((wr * FI + i) * 2) * 1024 + foff[kh]);
+#pragma unroll
+            for (int i = 0; i < FI; ++i)
+#pragma unroll
+                for (int j = 0; j < FJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    // epilogue: lane l holds rows 4*(l/16) + reg, column l % 16 of each block
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+        const int col = n0 + (wc * FJ + j) * 16 + (lane & 15);
+        const float b = col < N ? bias[col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < FI; ++i) {
+            const int rowb = m0 + (wr * FI + i) * 16 + 4 * (lane >> 4);
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg) {
+                const int row = rowb + rg;
+                float v = acc[i][j][rg] + b;
                 if (PRELU) v = (v < 0.0f) ? a * v : v;
-                y[c] = v;
+                if (row < M && col < N) __builtin_nontemporal_store(v, Y + (size_t)row * ldy + col);
             }
         }
     }
@@ -250,11 +343,12 @@ hipError_t csc_copy(const int* csp, const int* csn, const int* rip, const int* r
 }
 
 hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int rows,
-                         int ncols, float* wf, uint16_t* w3, long long n_pos, long long n_neg, int* bad,
+                         int ncols, float* wf, uint16_t* w3, int ldk, long long n_pos, long long n_neg, int* bad,
                          hipStream_t st) {
     const long long n = (long long)rows * ncols;
     hipError_t e = hipMemsetAsync(wf, 0, (size_t)n * sizeof(float), st);
     if (e != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w3, 0, (size_t)ncols * ldk * sizeof(uint16_t), st)) != hipSuccess) return e;
     const int wpb = 4;  // waves (columns) per block
     if (n_pos > 0)
         hipLaunchKernelGGL(k_w_scatter, dim3((ncols + wpb - 1) / wpb), dim3(64 * wpb), 0, st, csp, rip, col_begin,
@@ -262,56 +356,60 @@ hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const i
     if (n_neg > 0)
         hipLaunchKernelGGL(k_w_scatter, dim3((ncols + wpb - 1) / wpb), dim3(64 * wpb), 0, st, csn, rin, col_begin,
                            ncols, rows, -1.0f, wf);
-    hipLaunchKernelGGL(k_w3_from, dim3(grid_of(n, 256)), dim3(256), 0, st, wf, ncols, rows, w3, bad);
+    hipLaunchKernelGGL(k_w3_from, dim3(grid_of(n, 256)), dim3(256), 0, st, wf, ncols, rows, w3, ldk, bad);
     return hipGetLastError();
 }
 
-hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int* flags, int* any, int gen, hipStream_t st) {
-    const long long total = (long long)M * ((K + 3) / 4);
-    hipLaunchKernelGGL(k_split3, dim3(grid_of(total, 256)), dim3(256), 0, st, X, M, K, x3, flags, any, gen);
+hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int* flags, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_split3, dim3(M), dim3(256), 0, st, X, M, K, x3, ldk, flags);
     return hipGetLastError();
 }
 
-hipError_t mfma_epilogue_fix(const uint16_t* x3, int M, int K, const int* cp, const int* cn, const int* crp,
-                             const int* crn, int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu,
-                             float a, const int* flags, const int* any, int gen, hipStream_t st) {
-    const long long total = (long long)M * ((ncols + 3) / 4);
-    const dim3 grid(grid_of(total, 256)), block(256);
-#define TCSC_EPI_ARGS Y, M, ncols, ldy, B, a, x3, K, cp, cn, crp, crn, flags, any, gen
-    if (bias_first) {
-        if (prelu)
-            hipLaunchKernelGGL((k_epilogue_fix<true, true>), grid, block, 0, st, TCSC_EPI_ARGS);
-        else
-            hipLaunchKernelGGL((k_epilogue_fix<true, false>), grid, block, 0, st, TCSC_EPI_ARGS);
+// Tile choice: 256 x 256 (8 waves) unless that grid would leave more than
+// half of the 256 CUs idle, then 128 x 128 (4 waves).
+template <bool PRELU>
+static hipError_t launch_gemm3_t(const uint16_t* x3, const uint16_t* w3, int ldk, int M, int N, const float* B,
+                                 float* Y, int ldy, float a, hipStream_t st) {
+    const int ksteps = ldk / 64;
+    const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
+    if (big >= 128) {
+        const int tm = (M + 255) / 256, tn = (N + 255) / 256;
+        hipLaunchKernelGGL((k_gemm3<2, 4, 8, 4, PRELU>), dim3(tm * tn), dim3(512), 0, st, x3, w3, ldk, M, N, ksteps,
+                           B, Y, ldy, a, tm, tn);
     } else {
-        if (prelu)
-            hipLaunchKernelGGL((k_epilogue_fix<false, true>), grid, block, 0, st, TCSC_EPI_ARGS);
-        else
-            hipLaunchKernelGGL((k_epilogue_fix<false, false>), grid, block, 0, st, TCSC_EPI_ARGS);
+        const int tm = (M + 127) / 128, tn = (N + 127) / 128;
+        hipLaunchKernelGGL((k_gemm3<2, 2, 4, 4, PRELU>), dim3(tm * tn), dim3(256), 0, st, x3, w3, ldk, M, N, ksteps,
+                           B, Y, ldy, a, tm, tn);
     }
-#undef TCSC_EPI_ARGS
     return hipGetLastError();
 }
 
-hipError_t mfma_fixup(const uint16_t* x3, int M, int K, const int* cp, const int* cn, const int* crp, const int* crn,
-                      int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
-                      const int* flags, const int* any, int gen, hipStream_t st) {
+hipError_t mfma_gemm3(const uint16_t* x3, const uint16_t* w3, int ldk, int M, int N, const float* B, float* Y,
+                      int ldy, bool prelu, float a, hipStream_t st) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    if (ldk % 64 != 0) return hipErrorInvalidValue;
+    return prelu ? launch_gemm3_t<true>(x3, w3, ldk, M, N, B, Y, ldy, a, st)
+                 : launch_gemm3_t<false>(x3, w3, ldk, M, N, B, Y, ldy, a, st);
+}
+
+hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cp, const int* cn, const int* crp,
+                      const int* crn, int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu,
+                      float a, const int* flags, hipStream_t st) {
     const dim3 grid((ncols + 255) / 256), block(256);
+#define TCSC_FIX_ARGS x3, M, K, ldk, cp, cn, crp, crn, ncols, B, Y, ldy, a, flags
     if (bias_first) {
         if (prelu)
-            hipLaunchKernelGGL((k_fixup<true, true>), grid, block, 0, st, x3, M, K, cp, cn, crp, crn, ncols, B, Y, ldy,
-                               a, flags, any, gen);
+            hipLaunchKernelGGL((k_fixup<true, true>), grid, block, 0, st, TCSC_FIX_ARGS);
         else
-            hipLaunchKernelGGL((k_fixup<true, false>), grid, block, 0, st, x3, M, K, cp, cn, crp, crn, ncols, B, Y,
-                               ldy, a, flags, any, gen);
+            hipLaunchKernelGGL((k_fixup<true, false>), grid, block, 0, st, TCSC_FIX_ARGS);
     } else {
         if (prelu)
-            hipLaunchKernelGGL((k_fixup<false, true>), grid, block, 0, st, x3, M, K, cp, cn, crp, crn, ncols, B, Y,
-                               ldy, a, flags, any, gen);
+            hipLaunchKernelGGL((k_fixup<false, true>), grid, block, 0, st, TCSC_FIX_ARGS);
         else
-            hipLaunchKernelGGL((k_fixup<false, false>), grid, block, 0, st, x3, M, K, cp, cn, crp, crn, ncols, B, Y,
-                               ldy, a, flags, any, gen);
+            hipLaunchKernelGGL((k_fixup<false, false>), grid, block, 0, st, TCSC_FIX_ARGS);
     }
+#undef TCSC_FIX_ARGS
     return hipGetLastError();
 }
 

@@ -2,8 +2,7 @@
 workspace covers M, a launch allocates nothing and never synchronises, so it
 may be captured).  Replays must give the eager launch's bits on every path:
 the gather (k_transpose + k_stream), split-K (+ k_reduce), the small-M path
-and the MFMA path (one eager launch first: the BLAS library may allocate on
-its first call)."""
+and the MFMA path (k_split3 + k_gemm3 + k_fixup)."""
 import numpy as np
 import pytest
 
@@ -50,6 +49,53 @@ def test_graph_replay_bit_identical(torch_gpu, oracle, M, K, N, density, variant
         g.replay()
         torch.cuda.synchronize()
         np.testing.assert_array_equal(Yg.cpu().numpy().view(np.uint32), Ye.cpu().numpy().view(np.uint32))
+    del g
+    plan.destroy()
+    W.free()
+
+
+def test_graph_replay_mfma_path_with_and_without_special_rows(torch_gpu, oracle):
+    """the MFMA path's row flags must not carry over between
+    replays.  One captured launch, replayed on X holding inf / NaN / tiny
+    values (flagged rows, recomputed exactly), then on X without them, then
+    with them again: every replay equals the eager launch on the same X, bit
+    for bit."""
+    torch = torch_gpu
+    dev = torch.device("cuda:0")
+    M, K, N = 256, 1024, 512
+    Wd = oracle.ternary((K, N), 0.5, 950)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    plain = oracle.uniform((M, K), 951)
+    special = plain.copy()
+    special[3, 5] = np.inf
+    special[100, 7] = np.nan
+    special[200, 9] = 1e-35
+    B = torch.from_numpy(oracle.uniform((N,), 952)).to(dev)
+    side = torch.cuda.Stream()
+    plan = tcsc_amd.Plan(W, 0, N, 0, side.cuda_stream)
+    plan.reserve(M)
+    assert plan.info()["mfma_min_M"] and M >= plan.info()["mfma_min_M"]
+    X = torch.empty((M, K), device=dev)
+    eager = {}
+    for name, x in (("plain", plain), ("special", special)):
+        X.copy_(torch.from_numpy(x))
+        Ye = torch.empty((M, N), device=dev)
+        with torch.cuda.stream(side):
+            plan.sgemm(X, B, Ye, M, N, "prelu_basic", 0.2, side.cuda_stream)
+        side.synchronize()
+        eager[name] = Ye.cpu().numpy().view(np.uint32).copy()
+    assert not np.array_equal(eager["plain"], eager["special"])
+    Yg = torch.empty((M, N), device=dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        plan.sgemm(X, B, Yg, M, N, "prelu_basic", 0.2, torch.cuda.current_stream().cuda_stream)
+    for name in ("special", "plain", "special", "plain"):
+        X.copy_(torch.from_numpy(special if name == "special" else plain))
+        Yg.fill_(float("nan"))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(Yg.cpu().numpy().view(np.uint32), eager[name], err_msg=name)
     del g
     plan.destroy()
     W.free()

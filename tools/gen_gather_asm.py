@@ -266,7 +266,7 @@ def write_inc(path, g):
     ndw = g.hdr + 2 * g.cap      # scalar buffer: header + entries
     nsv = ndw // 16              # 16-SGPR vectors of the buffer
     stail = ndw % 16             # + one 4- or 8-SGPR vector
-    assert stail in (0, 4, 8)
+    assert stail in (0, 4, 8, 12)
     with open(path, "w") as f:
         f.write("// GENERATED by tools/gen_gather_asm.py -- do not edit by hand.\n")
         f.write(f"// geometry: cw={g.cw} batch={g.batch} cap={g.cap} vgpr budget={g.budget} depth={g.depth} "
