@@ -36,7 +36,10 @@ constexpr int kWavesPerSimd = kWaves / 4;
 static_assert(kWaves % 4 == 0 && kWaves <= 16, "whole waves per SIMD");
 constexpr int kEntGuard = 64;            // entries allocated past the last stream (empty chain + block loads)
 constexpr int kHdr = 2;                  // header entries ahead of every (group, chunk) stream
-constexpr int kLdsBytes = kNBuf * kBufRows * kRowBytes;  // 147 KiB
+constexpr int kRingBytes = kNBuf * kBufRows * kRowBytes;  // 147 KiB
+// the epilogue parks 64 rows x (kCW*4 + 16) B per wave at least
+constexpr int kEpiMinBytes = kWaves * 64 * (kCW * 4 + 16);
+constexpr int kLdsBytes = kRingBytes > kEpiMinBytes ? kRingBytes : kEpiMinBytes;
 // Staging: waves 0..kDmaWaves-1 move a chunk, kDmaPerWave 1-KiB rows each,
 // right after the chunk loop's barrier (TCSC_DMA_EARLY=1) or after their
 // gather (0).  Default: the first half of the waves.  The SIMD arbiter
@@ -54,7 +57,7 @@ constexpr bool kDmaEarly = TCSC_DMA_EARLY != 0;
 constexpr int kDmaPerWave = kTK / kDmaWaves;              // 1-KiB LDS-DMA rows per DMA wave and chunk
 static_assert(kDmaWaves <= kWaves && kTK % kDmaWaves == 0, "each DMA wave moves the same number of rows");
 static_assert(kLdsBytes <= 160 * 1024, "LDS");
-static_assert(kNBuf == 2 || kNBuf == 3, "ring of 2 (DMA(c+1) before gather(c)) or 3 (DMA(c+2) after it)");
+static_assert(kNBuf >= 2 && kNBuf <= 5, "ring of 2 (DMA(c+1) before gather(c)) or n >= 3 (DMA(c+n-1) after it)");
 
 // Stream layout (v4).  Group-major: the streams of one wave-column group
 // follow each other chunk by chunk, each behind a header of kHdr entries

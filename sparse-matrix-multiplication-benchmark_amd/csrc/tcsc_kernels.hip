@@ -526,45 +526,25 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         i32x16 sb[TCSC_SBUF_VECS];
         sbuf_tail_t sbt;
         load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
-        if (kNBuf == 3 && dma_wave) dma_next_chunk(dma, buf0 == 2 ? 0 : buf0 + 1);  // DMA(c_begin+1)
+        // DMA(c_begin+1 .. c_begin+kNBuf-2): a ring of n keeps n-1 chunks in flight
+#pragma unroll
+        for (int i = 1; i + 1 < kNBuf; ++i)
+            if (dma_wave) dma_next_chunk(dma, (buf0 + i) % kNBuf);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                       // pad rows
 
         const unsigned mask = 0x3ffu;
-#if defined(TCSC_ABLATION) && TCSC_ABLATION == 7
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const unsigned long long cur0 = cur;
-        i32x16 sb_first[TCSC_SBUF_VECS];
-#pragma unroll
-        for (int i = 0; i < TCSC_SBUF_VECS; ++i) sb_first[i] = sb[i];
-        const sbuf_tail_t sbt_first = sbt;
-#endif
         // ring buffer that DMA(c+2) (ring of 3) / DMA(c+1) (ring of 2) fills
-        int dbuf = kNBuf == 3 ? (buf0 == 0 ? 2 : buf0 - 1) : (buf0 ^ 1);
+        int dbuf = kNBuf >= 3 ? (buf0 + kNBuf - 1) % kNBuf : (buf0 ^ 1);
         for (int c = c_begin; c < c_end; ++c) {
             // see the VMEM order above: ring of 3 keeps DMA(c+1) in flight
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kNBuf == 3 ? kDmaPerWave : 0) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kNBuf >= 3 ? (kNBuf - 2) * kDmaPerWave : 0) : "memory");
             __builtin_amdgcn_s_barrier();
             if ((kNBuf == 2 || kDmaEarly) && dma_wave) dma_next_chunk(dma, dbuf);
-#if defined(TCSC_ABLATION) && TCSC_ABLATION == 7
-            // timing only (wrong results): every chunk replays the first chunk's
-            // stream from the SGPR buffer loaded before the loop -- the chunk
-            // loop with no scalar stream load per chunk
-            {
-                const unsigned long long first = cur0;
-                i32x16 sb0[TCSC_SBUF_VECS];
-                sbuf_tail_t sbt0 = sbt_first;
-#pragma unroll
-                for (int i = 0; i < TCSC_SBUF_VECS; ++i) sb0[i] = sb_first[i];
-                unsigned long long p0 = first;
-                gather_stream(sb0, sbt0, p0, lane, mask, acc);
-            }
-#else
             gather_stream(sb, sbt, cur, lane, mask, acc);  // leaves cur at the next chunk's header
             // next chunk's stream: lands behind the DMA issue and the barrier
             load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
-#endif
             // DMA(c+2) into the buffer chunk c-1 used
-            if (kNBuf == 3 && !kDmaEarly && dma_wave) dma_next_chunk(dma, dbuf);
+            if (kNBuf >= 3 && !kDmaEarly && dma_wave) dma_next_chunk(dma, dbuf);
             dbuf = dbuf == kNBuf - 1 ? 0 : dbuf + 1;
         }
         // no LDS-DMA may still be writing when the workgroup's LDS is
