@@ -431,6 +431,22 @@ __device__ __forceinline__ Tile xcd_tile() {
     return t;
 }
 
+#ifdef TCSC_STAMPS
+// Diagnostic build only (make lib/abl/libtcsc_amd_stamps.so): per wave, the
+// chunk loop's cycles summed by segment -- gather, post-gather (stream load
+// + DMA issue, waited for), top-of-chunk (vmcnt + barrier) -- and its total;
+// read with tcsc_debug_stamps().  Stamps never feed an output.
+constexpr int kStampWgs = 4096;
+__device__ unsigned long long g_stamps[kStampWgs * kWaves * 4];
+__device__ __forceinline__ unsigned long long stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#endif
+
 // OUT: 0 = final Y (bias + activation), 1 = partial slab ws[slice][M][ncols]
 // ORDER (the summation order, DESIGN.md "Numerics"):
 //   0  one plan, each column's +1 and -1 entries merged by ascending k;
@@ -535,18 +551,44 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         const unsigned mask = 0x3ffu;
         // ring buffer that DMA(c+2) (ring of 3) / DMA(c+1) (ring of 2) fills
         int dbuf = kNBuf >= 3 ? (buf0 + kNBuf - 1) % kNBuf : (buf0 ^ 1);
+#ifdef TCSC_STAMPS
+        unsigned long long st_g = 0, st_p = 0, st_w = 0, t2 = stamp();
+        const unsigned long long t_begin = t2;
+#endif
         for (int c = c_begin; c < c_end; ++c) {
             // see the VMEM order above: ring of 3 keeps DMA(c+1) in flight
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kNBuf >= 3 ? (kNBuf - 2) * kDmaPerWave : 0) : "memory");
             __builtin_amdgcn_s_barrier();
+#ifdef TCSC_STAMPS
+            const unsigned long long t0 = stamp();
+            st_w += t0 - t2;
+#endif
             if ((kNBuf == 2 || kDmaEarly) && dma_wave) dma_next_chunk(dma, dbuf);
             gather_stream(sb, sbt, cur, lane, mask, acc);  // leaves cur at the next chunk's header
+#ifdef TCSC_STAMPS
+            const unsigned long long t1 = stamp();
+            st_g += t1 - t0;
+#endif
             // next chunk's stream: lands behind the DMA issue and the barrier
             load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
             // DMA(c+2) into the buffer chunk c-1 used
             if (kNBuf >= 3 && !kDmaEarly && dma_wave) dma_next_chunk(dma, dbuf);
             dbuf = dbuf == kNBuf - 1 ? 0 : dbuf + 1;
+#ifdef TCSC_STAMPS
+            t2 = stamp();  // waits for the stream load too
+            st_p += t2 - t1;
+#endif
         }
+#ifdef TCSC_STAMPS
+        if (lane == 0) {
+            const int wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+            unsigned long long* o = g_stamps + ((size_t)(wg % kStampWgs) * kWaves + wave) * 4;
+            o[0] = st_g;
+            o[1] = st_p;
+            o[2] = st_w;
+            o[3] = t2 - t_begin;
+        }
+#endif
         // no LDS-DMA may still be writing when the workgroup's LDS is
         // released, and the last (unused) stream load must have landed
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1128,6 +1170,12 @@ hipError_t exclusive_scan_i32(const int* in, int* out, int n, void* tmp, size_t 
 }
 
 int ldxt_for(int M) { return ldxt_of(M); }
+
+#ifdef TCSC_STAMPS
+extern "C" __attribute__((visibility("default"))) int tcsc_debug_stamps(void* dst, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps), bytes < sizeof(g_stamps) ? bytes : sizeof(g_stamps));
+}
+#endif
 
 hipError_t launch_transpose(const float* X, int M, int K, float* XT, int ldxt, hipStream_t st) {
     if (M <= 0 || K <= 0) return hipSuccess;
