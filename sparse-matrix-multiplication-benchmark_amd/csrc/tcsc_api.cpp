@@ -133,7 +133,7 @@ int build_plan(int rows, int col_begin, int ncols, long long n_pos, long long n_
     plan->n_pos = n_pos;
     plan->n_neg = n_neg;
     plan->n_chunks = rows > 0 ? (rows + tcsc::kTK - 1) / tcsc::kTK : 0;
-    plan->n_groups = (ncols + tcsc::kCW - 1) / tcsc::kCW;
+    plan->n_groups = tcsc::groups_for(ncols);
     const int nch = plan->n_chunks, G = plan->n_groups;
     const long long nc = (long long)nch * ncols, ng = (long long)nch * G;
     if (n_pos + n_neg > 0x3fffffffLL || nc + 1 > 0x7fffffffLL || ng + 1 > 0x7fffffffLL) {

@@ -30,10 +30,53 @@ constexpr int kBufRows = kTK + 1;        // + one row of -0.0 that padding entri
 #define TCSC_BATCH 4
 #endif
 constexpr int kWaves = TCSC_WAVES;       // waves per workgroup (1 workgroup per CU; kWaves/4 per SIMD)
-constexpr int kCW = TCSC_CW;             // output columns per wave (4*kCW accumulator VGPRs)
+constexpr int kCW = TCSC_CW;             // most output columns of one wave (4*kCW accumulator VGPRs)
 constexpr int kBatch = TCSC_BATCH;       // stream entries per batch (pipeline step, stream padding)
 constexpr int kWavesPerSimd = kWaves / 4;
 static_assert(kWaves % 4 == 0 && kWaves <= 16, "whole waves per SIMD");
+
+// Output columns per wave, by the wave's age rank on its SIMD (waves 4r ..
+// 4r+3 have rank r; one wave of every rank runs on each SIMD).  The SIMD's
+// instruction arbiter favours older waves: with equal shares the youngest
+// rank finishes its gather last (tools/stamps.py: gather cycles per chunk
+// 835 / 967 / 1330 / 1600 by rank at cfg 4).  Unequal shares were measured
+// slower in either direction (make lib/wid/libtcsc_amd_wd<A>_<B>_<C>_<D>.so,
+// DESIGN.md §4), so the default is equal.  Multiples of 4 (16-B epilogue
+// stores), at most kCW.
+#ifndef TCSC_WIDTHS
+#define TCSC_WIDTHS 16, 16, 16, 16
+#endif
+struct ColLayout {
+    int w[kWavesPerSimd];
+};
+constexpr ColLayout kRankCols{{TCSC_WIDTHS}};
+__host__ __device__ constexpr int wave_cols(int w) { return kRankCols.w[w >> 2]; }
+__host__ __device__ constexpr int wave_col0(int w) {
+    int s = 0;
+    for (int r = 0; r < (w >> 2); ++r) s += 4 * kRankCols.w[r];
+    return s + (w & 3) * kRankCols.w[w >> 2];
+}
+constexpr int wg_cols() {
+    int s = 0;
+    for (int r = 0; r < kWavesPerSimd; ++r) s += 4 * kRankCols.w[r];
+    return s;
+}
+constexpr int kWgCols = wg_cols();  // columns of one workgroup (column block)
+constexpr bool widths_ok() {
+    for (int r = 0; r < kWavesPerSimd; ++r)
+        if (kRankCols.w[r] <= 0 || kRankCols.w[r] > kCW || kRankCols.w[r] % 4) return false;
+    return true;
+}
+static_assert(widths_ok(), "TCSC_WIDTHS: one width per rank, multiples of 4, at most TCSC_CW");
+// Wave-column group g = column block g / kWaves, wave g % kWaves.
+__host__ __device__ constexpr int group_col0(int g) { return (g / kWaves) * kWgCols + wave_col0(g % kWaves); }
+__host__ __device__ constexpr int group_cols(int g) { return wave_cols(g % kWaves); }
+// groups with at least one of ncols columns (group_col0 ascends with g)
+__host__ __device__ constexpr int groups_for(int ncols) {
+    int g = (ncols / kWgCols) * kWaves;
+    while (group_col0(g) < ncols) ++g;
+    return g;
+}
 constexpr int kEntGuard = 64;            // entries allocated past the last stream (empty chain + block loads)
 constexpr int kHdr = 2;                  // header entries ahead of every (group, chunk) stream
 constexpr int kRingBytes = kNBuf * kBufRows * kRowBytes;  // 147 KiB
@@ -87,7 +130,7 @@ struct PlanDev {
 // Plan arrays (device).  Everything but ent/sptr is build-time scratch.
 struct PlanOut {
     int n_chunks = 0;
-    int n_groups = 0;          // ceil(ncols / kCW) wave-column groups
+    int n_groups = 0;          // groups_for(ncols) wave-column groups
     long long n_entries = 0;   // stream entries incl. padding
     int2* ent = nullptr;       // n_entries (+kBatch) entries
     int* sptr = nullptr;       // n_groups*n_chunks + 1 header positions (entries), group-major

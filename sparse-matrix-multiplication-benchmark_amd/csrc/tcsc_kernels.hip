@@ -41,14 +41,17 @@
 
 namespace tcsc {
 
-typedef float f32x32 __attribute__((ext_vector_type(32)));
-
 // The generated gather loop (tools/gen_gather_asm.py) and its geometry.
 #ifdef TCSC_GATHER_INC
 #include TCSC_GATHER_INC
 #else
 #include "gather_asm.inc"
 #endif
+#ifndef TCSC_ACC_W
+#define TCSC_ACC_W 32
+#endif
+// accumulator registers in TCSC_ACC_VECS vectors of TCSC_ACC_W (the generated asm operands)
+typedef float facc_t __attribute__((ext_vector_type(TCSC_ACC_W)));
 static_assert(TCSC_GEN_CW == kCW && TCSC_GEN_BATCH == kBatch, "generated loop geometry");
 static_assert(TCSC_GEN_CAP + kHdr <= kEntGuard, "stream prefetch stays inside the entry guard");
 static_assert(TCSC_GEN_HDR == 2 * kHdr, "generated loop and plan agree on the chunk header");
@@ -115,7 +118,7 @@ __global__ void k_group_counts(const int* __restrict__ cptr, int ncols, int nch,
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
          i += (long long)gridDim.x * blockDim.x) {
         const int g = (int)(i / nch), c = (int)(i % nch);
-        const int n0 = g * kCW, n1 = min(n0 + kCW, ncols);
+        const int n0 = group_col0(g), n1 = min(n0 + group_cols(g), ncols);
         const int real = cptr[(long long)c * ncols + n1] - cptr[(long long)c * ncols + n0];
         gcnt[i] = kHdr + (real + kPad - 1) / kPad * kPad;
     }
@@ -151,11 +154,12 @@ __global__ void k_scatter(const int* __restrict__ cs_own, const int* __restrict_
         const int k = ri_own[i];
         const int c = k / kTK;
         const long long b = (long long)c * ncols + n;
-        const int g = n / kCW, j = n - g * kCW;
+        int g = (n / kWgCols) * kWaves, j = n - (n / kWgCols) * kWgCols;  // group of column n, its slot
+        while (j >= wave_cols(g % kWaves)) j -= wave_cols(g++ % kWaves);
         const int rank_own = i - lb_own[b];
         const int rank_oth = (SIGN ? upper_bound_i32(ri_oth, cs_oth[gn], cs_oth[gn + 1], k)
                                    : lower_bound_i32(ri_oth, cs_oth[gn], cs_oth[gn + 1], k)) - lb_oth[b];
-        const int in_group = cptr[b] - cptr[(long long)c * ncols + g * kCW];
+        const int in_group = cptr[b] - cptr[(long long)c * ncols + group_col0(g)];
         const int pos = sptr[(long long)g * (ent_nch) + c] + kHdr + in_group + rank_own + rank_oth;
         ent[pos] = make_int2(sgn, (lds_row_of(c, k - c * kTK) << 10) | (4 * j));
     }
@@ -174,7 +178,7 @@ __global__ void k_fill_headers(const int* __restrict__ cptr, const int* __restri
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
          i += (long long)gridDim.x * blockDim.x) {
         const int g = (int)(i / nch), c = (int)(i % nch);
-        const int n0 = g * kCW, n1 = min(n0 + kCW, ncols);
+        const int n0 = group_col0(g), n1 = min(n0 + group_cols(g), ncols);
         const int real = cptr[(long long)c * ncols + n1] - cptr[(long long)c * ncols + n0];
         const int s0 = sptr[i], s1 = sptr[i + 1];
         const int n = s1 - s0 - kHdr;
@@ -300,7 +304,7 @@ static_assert(TCSC_GEN_TOUCH == 0, "the chunk loop passes no scalar-cache touch 
 // The schedule and register map are in tools/gen_gather_asm.py.
 __device__ __forceinline__ void gather_stream(i32x16 (&sb)[TCSC_SBUF_VECS], sbuf_tail_t& sbt,
                                               unsigned long long& ptr, unsigned lane, unsigned mask,
-                                              f32x32 (&acc)[TCSC_ACC_VECS]) {
+                                              facc_t (&acc)[TCSC_ACC_VECS]) {
     (void)sbt;
 #if defined(TCSC_GEN_PF) && TCSC_GEN_PF
     int junk = 0;  // destination of the reload prefetch (tools/gen_gather_asm.py --pf)
@@ -327,8 +331,8 @@ __device__ __forceinline__ void load_stream(i32x16 (&sb)[TCSC_SBUF_VECS], sbuf_t
 }
 
 // i is a compile-time constant after unrolling
-__device__ __forceinline__ float acc_get(const f32x32 (&acc)[TCSC_ACC_VECS], int i) { return acc[i >> 5][i & 31]; }
-__device__ __forceinline__ void acc_set(f32x32 (&acc)[TCSC_ACC_VECS], int i, float v) { acc[i >> 5][i & 31] = v; }
+__device__ __forceinline__ float acc_get(const facc_t (&acc)[TCSC_ACC_VECS], int i) { return acc[i / TCSC_ACC_W][i % TCSC_ACC_W]; }
+__device__ __forceinline__ void acc_set(facc_t (&acc)[TCSC_ACC_VECS], int i, float v) { acc[i / TCSC_ACC_W][i % TCSC_ACC_W] = v; }
 
 // LDS-DMA of X^T chunks.  Row k of chunk c = XT[c*kTK + k][m0..m0+255] (1
 // KiB); wave w moves rows w*D .. w*D+D-1 (D = kDmaPerWave), lane l the 16 B
@@ -477,16 +481,16 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     const int c_end = min(nch, c_begin + chunks_per_slice);
     const bool active = g < G;
 
-    f32x32 acc[TCSC_ACC_VECS];
+    facc_t acc[TCSC_ACC_VECS];
 #pragma unroll
     for (int v = 0; v < TCSC_ACC_VECS; ++v)
 #pragma unroll
-        for (int i = 0; i < 32; ++i) acc[v][i] = 0.f;
+        for (int i = 0; i < TCSC_ACC_W; ++i) acc[v][i] = 0.f;
     if (BIAS_FIRST && OUT == 0 && active) {
-        // one vector load of the wave's kCW bias values, then lane broadcasts
+        // one vector load of the wave's bias values, then lane broadcasts
         // (keeps them out of the SGPRs the gather loop owns)
-        const int cb = g * kCW + lane;
-        const float bv = (lane < kCW && cb < ncols) ? Bias[cb] : 0.f;
+        const int cb = group_col0(g) + lane;
+        const float bv = (lane < wave_cols(wave) && cb < ncols) ? Bias[cb] : 0.f;
 #pragma unroll
         for (int j = 0; j < kCW; ++j) {
             const float b = __shfl(bv, j);
@@ -615,7 +619,8 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         constexpr int kLanesPerPass = kEpiRows / 4;
         constexpr int kRowsPerRead = 64 / kQ;       // rows one read instruction covers
         char* region = lds + wave * (kEpiRows * kStride);
-        const int col0 = g * kCW;
+        const int col0 = group_col0(g);
+        const int col_end = min(col0 + wave_cols(wave), ncols);  // this wave's columns: [col0, col_end)
         const bool vec_ok = OUT == 0 ? ((ldy & 3) == 0 && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0))
                                      : ((ncols & 3) == 0 && ((reinterpret_cast<uintptr_t>(ws) & 15) == 0));
         constexpr bool kAddBias = OUT == 0 && (HOW == 1 || (HOW == 0 && !BIAS_FIRST));
@@ -642,10 +647,10 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                 const int col = col0 + 4 * q;
                 float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (kAddBias) {
-                    bq.x = col + 0 < ncols ? Bias[col + 0] : 0.f;
-                    bq.y = col + 1 < ncols ? Bias[col + 1] : 0.f;
-                    bq.z = col + 2 < ncols ? Bias[col + 2] : 0.f;
-                    bq.w = col + 3 < ncols ? Bias[col + 3] : 0.f;
+                    bq.x = col + 0 < col_end ? Bias[col + 0] : 0.f;
+                    bq.y = col + 1 < col_end ? Bias[col + 1] : 0.f;
+                    bq.z = col + 2 < col_end ? Bias[col + 2] : 0.f;
+                    bq.w = col + 3 < col_end ? Bias[col + 3] : 0.f;
                 }
 #pragma unroll 4
                 for (int i = 0; i < (kEpiRows + kRowsPerRead - 1) / kRowsPerRead; ++i) {
@@ -653,16 +658,16 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                     const int row = m0 + kEpiRows * h + R;
                     if (R >= kEpiRows) break;
                     float4 v = *reinterpret_cast<const float4*>(region + R * kStride + q * 16);
-                    if (row < M && col < ncols) {
+                    if (row < M && col < col_end) {
                         float* dst;
                         if (OUT == 0) {
                             dst = Y + (size_t)row * ldy + col;
                             if (HOW == 2) {  // the parked bias + (+1 sums), then + (-1 sums)
-                                const bool full = vec_ok && col + 3 < ncols;
+                                const bool full = vec_ok && col + 3 < col_end;
                                 v.x = dst[0] + v.x;
-                                v.y = (full || col + 1 < ncols) ? dst[1] + v.y : v.y;
-                                v.z = (full || col + 2 < ncols) ? dst[2] + v.z : v.z;
-                                v.w = (full || col + 3 < ncols) ? dst[3] + v.w : v.w;
+                                v.y = (full || col + 1 < col_end) ? dst[1] + v.y : v.y;
+                                v.z = (full || col + 2 < col_end) ? dst[2] + v.z : v.z;
+                                v.w = (full || col + 3 < col_end) ? dst[3] + v.w : v.w;
                             }
                             if (kAddBias) {
                                 v.x += bq.x;
@@ -679,7 +684,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                         } else {
                             dst = ws + ((size_t)t.z * M + row) * ncols + col;
                         }
-                        if (vec_ok && col + 3 < ncols) {
+                        if (vec_ok && col + 3 < col_end) {
                             if (OUT == 0 && HOW != 1) {  // Y is never re-read here: keep it out of L2's way
                                 typedef float nt4 __attribute__((ext_vector_type(4)));
                                 nt4 w = {v.x, v.y, v.z, v.w};
@@ -689,9 +694,9 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                             }
                         } else {
                             dst[0] = v.x;
-                            if (col + 1 < ncols) dst[1] = v.y;
-                            if (col + 2 < ncols) dst[2] = v.z;
-                            if (col + 3 < ncols) dst[3] = v.w;
+                            if (col + 1 < col_end) dst[1] = v.y;
+                            if (col + 2 < col_end) dst[2] = v.z;
+                            if (col + 3 < col_end) dst[3] = v.w;
                         }
                     }
                 }
@@ -712,7 +717,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
 #pragma unroll
         for (int v = 0; v < TCSC_ACC_VECS; ++v)
 #pragma unroll
-            for (int i = 0; i < 32; ++i) acc[v][i] = 0.f;
+            for (int i = 0; i < TCSC_ACC_W; ++i) acc[v][i] = 0.f;
         __syncthreads();  // the epilogue's LDS staging is done before the ring is refilled
         pad_rows();
         run_chain(ent2, sptr2, n_entries2);

@@ -55,7 +55,7 @@ import sys
 
 class Geo:
     def __init__(self, cw, batch, cap, budget, depth=1, touch=4, tail=1, hdr=4, pf=0):
-        assert cw % 8 == 0 and cap % batch == 0 and 36 + hdr + 2 * cap <= 100
+        assert cw % 4 == 0 and cap % batch == 0 and 36 + hdr + 2 * cap <= 100
         assert hdr == 4 and (hdr + 2 * cap) % 4 == 0
         assert 1 <= depth and depth * batch <= 15, "lgkmcnt counts to 15"
         self.cw, self.batch, self.cap, self.budget, self.depth = cw, batch, cap, budget, depth
@@ -262,7 +262,8 @@ def emit(f, name, lines):
 
 def write_inc(path, g):
     global ABL
-    nvec = 4 * g.cw // 32
+    aw = 32 if (4 * g.cw) % 32 == 0 else 16  # accumulator vector width (asm operands)
+    nvec = 4 * g.cw // aw
     ndw = g.hdr + 2 * g.cap      # scalar buffer: header + entries
     nsv = ndw // 16              # 16-SGPR vectors of the buffer
     stail = ndw % 16             # + one 4- or 8-SGPR vector
@@ -275,10 +276,10 @@ def write_inc(path, g):
                 f"stream s[{g.sbase}:{g.slast}]\n")
         f.write(f"#define TCSC_GEN_CW {g.cw}\n#define TCSC_GEN_BATCH {g.batch}\n#define TCSC_GEN_CAP {g.cap}\n")
         f.write(f"#define TCSC_GEN_HDR {g.hdr}\n")
-        f.write(f"#define TCSC_GEN_BUDGET {g.budget}\n#define TCSC_ACC_VECS {nvec}\n#define TCSC_SBUF_VECS {nsv}\n")
+        f.write(f"#define TCSC_GEN_BUDGET {g.budget}\n#define TCSC_ACC_W {aw}\n#define TCSC_ACC_VECS {nvec}\n#define TCSC_SBUF_VECS {nsv}\n")
         f.write(f"#define TCSC_SBUF_TAIL {stail}\n")
         f.write(f"#define TCSC_GEN_TAIL {int(g.tail)}\n")
-        ops = ", ".join(f'"+{{v[{g.acc + 32 * i}:{g.acc + 32 * i + 31}]}}"(acc[{i}])' for i in range(nvec))
+        ops = ", ".join(f'"+{{v[{g.acc + aw * i}:{g.acc + aw * i + aw - 1}]}}"(acc[{i}])' for i in range(nvec))
         f.write(f"#define TCSC_ACC_OPERANDS(acc) {ops}\n")
         sops = ", ".join(f'"+{{s[{g.sbuf + 16 * i}:{g.sbuf + 16 * i + 15}]}}"(sb[{i}])' for i in range(nsv))
         if stail:
