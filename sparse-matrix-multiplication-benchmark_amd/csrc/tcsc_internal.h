@@ -77,12 +77,27 @@ __host__ __device__ constexpr int groups_for(int ncols) {
     while (group_col0(g) < ncols) ++g;
     return g;
 }
-constexpr int kEntGuard = 64;            // entries allocated past the last stream (empty chain + block loads)
+// L2 prefetch of the entry streams: after every chunk each
+// wave touches `lines` 128-B lines of its own stream starting `dist` bytes
+// past the next chunk's header (one global_load_lds_dword into a 256-B
+// scratch per wave after the ring: it writes no VGPR and no SGPR, and counts
+// in vmcnt, not lgkmcnt, so the gather's counted LDS waits stay exact).  The
+// launcher picks dist and lines from the plan's stream bytes per chunk
+// (pf_stream_params).  TCSC_PF_S=0 builds without it.
+#ifndef TCSC_PF_S
+#define TCSC_PF_S 1
+#endif
+constexpr bool kPfS = TCSC_PF_S != 0;
+constexpr int kPfWindow = 1792;  // dist + 128 * lines at most (bytes)
+// entries allocated past the last stream (empty chain + block loads + the stream prefetch window)
+constexpr int kEntGuard = kPfS ? kPfWindow / 8 + 8 : 64;
+static_assert(kEntGuard <= 256, "k_fill_headers writes the guard with one block");
 constexpr int kHdr = 2;                  // header entries ahead of every (group, chunk) stream
 constexpr int kRingBytes = kNBuf * kBufRows * kRowBytes;  // 147 KiB
+constexpr int kPfScratch = kPfS ? kWaves * 256 : 0;  // prefetch landing area, 256 B per wave
 // the epilogue parks 64 rows x (kCW*4 + 16) B per wave at least
 constexpr int kEpiMinBytes = kWaves * 64 * (kCW * 4 + 16);
-constexpr int kLdsBytes = kRingBytes > kEpiMinBytes ? kRingBytes : kEpiMinBytes;
+constexpr int kLdsBytes = (kRingBytes + kPfScratch) > kEpiMinBytes ? (kRingBytes + kPfScratch) : kEpiMinBytes;
 // Staging: waves 0..kDmaWaves-1 move a chunk, kDmaPerWave 1-KiB rows each,
 // right after the chunk loop's barrier (TCSC_DMA_EARLY=1) or after their
 // gather (0).  Default: the first half of the waves.  The SIMD arbiter
@@ -177,6 +192,9 @@ hipError_t plan_counts(const PlanDev& in, PlanOut& out, hipStream_t st);    // -
 hipError_t plan_fill(const PlanDev& in, PlanOut& out, hipStream_t st);      // -> sptr, ent
 // Launch
 int choose_slices(int M, int ncols, int K, long long nnz, int n_groups, size_t ws_bytes, int force);
+// stream prefetch of a plan of n_entries entries over n_groups x n_chunks
+// streams: *dist bytes ahead, *lines 128-B lines (TCSC_PF_DIST / TCSC_PF_LINES override)
+void pf_stream_params(long long n_entries, int n_groups, int n_chunks, int* dist, int* lines);
 size_t workspace_bytes(int M, int ncols, int slices);
 size_t xt_bytes(int M, int K);
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st);

@@ -35,6 +35,9 @@
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <type_traits>
 
 #include "tcsc_internal.h"
@@ -187,8 +190,9 @@ __global__ void k_fill_headers(const int* __restrict__ cptr, const int* __restri
         const int2 pad = make_int2(0x3f800000, lds_row_of(c, kTK) << 10);
         for (int p = s0 + kHdr + real; p < s1; ++p) ent[p] = pad;
     }
-    if (blockIdx.x == 0 && threadIdx.x < kEntGuard)
-        ent[n_entries + threadIdx.x] = threadIdx.x < kHdr ? make_int2(0, 0) : make_int2(0x3f800000, kTK << 10);
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < kEntGuard; i += blockDim.x)
+            ent[n_entries + i] = i < kHdr ? make_int2(0, 0) : make_int2(0x3f800000, kTK << 10);
 }
 
 // Plan-build precondition on device-resident TCSC arrays, one thread per
@@ -412,6 +416,13 @@ __device__ __forceinline__ void dma_next_chunk(DmaState& d, int buf) {
     d.next += d.chunk_bytes;
 }
 
+// L2 prefetch of the entry stream (kPfS): one global_load_lds_dword per wave
+// and chunk into the wave's 256-B scratch; the data is never read.
+__device__ __forceinline__ void pf_touch(unsigned m0, unsigned voff, const char* base) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2" : : "s"(m0), "v"(voff), "s"(base)
+                 : "memory");
+}
+
 // XCD-aware tile order.  Workgroups are dealt round-robin over the 8 XCDs
 // (MI355X_MICROARCH.md "Workgroup dispatch"; speed only, never correctness),
 // so launch order L puts L % 8 on one XCD.  Renumber so each XCD gets a
@@ -469,7 +480,8 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd)
 k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __restrict__ ent,
          const int* __restrict__ sptr, long long n_entries, const int2* __restrict__ ent2,
          const int* __restrict__ sptr2, long long n_entries2, int G, int ncols, int nch, int chunks_per_slice,
-         const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a, float* __restrict__ ws) {
+         const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a, float* __restrict__ ws, int pf_dist,
+         int pf_lines) {
     static_assert(ORDER == 0 || OUT == 0, "the reference orders do not split K");
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const int lane = threadIdx.x & 63;
@@ -536,6 +548,16 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         dma.lds_wave = (unsigned)reinterpret_cast<uintptr_t>(lds) + (unsigned)(wave * kDmaPerWave * kRowBytes);
         const bool dma_wave = wave < kDmaWaves;  // uniform
         const int buf0 = c_begin % kNBuf;
+        // stream prefetch (pf_stream_params): this wave's 256-B scratch and its lane offsets
+        const unsigned pf_m0 = (unsigned)reinterpret_cast<uintptr_t>(lds) + kRingBytes + 256u * wave;
+        // pf_lines is 1, 2, 4 or 8: lane groups of 64 / pf_lines lanes touch one line each
+        const unsigned pf_s_off = (unsigned)pf_dist + 128u * (unsigned)(lane * pf_lines >> 6);
+        // one stream prefetch right after every DMA issue (the prologue's
+        // included), so the top-of-chunk vmcnt count is the same for every
+        // chunk; `p` is the header of the next chunk to gather
+        auto pf_issue = [&](unsigned long long p) {
+            if (kPfS) pf_touch(pf_m0, pf_s_off, reinterpret_cast<const char*>(p));
+        };
         if (dma_wave) dma_next_chunk(dma, buf0);  // DMA(c_begin)
 
         // This wave's chain of chunk streams (stream layout v4,
@@ -546,10 +568,13 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         i32x16 sb[TCSC_SBUF_VECS];
         sbuf_tail_t sbt;
         load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
+        pf_issue(cur);
         // DMA(c_begin+1 .. c_begin+kNBuf-2): a ring of n keeps n-1 chunks in flight
 #pragma unroll
-        for (int i = 1; i + 1 < kNBuf; ++i)
+        for (int i = 1; i + 1 < kNBuf; ++i) {
             if (dma_wave) dma_next_chunk(dma, (buf0 + i) % kNBuf);
+            pf_issue(cur);
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                       // pad rows
 
         const unsigned mask = 0x3ffu;
@@ -561,7 +586,9 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
 #endif
         for (int c = c_begin; c < c_end; ++c) {
             // see the VMEM order above: ring of 3 keeps DMA(c+1) in flight
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kNBuf >= 3 ? (kNBuf - 2) * kDmaPerWave : 0) : "memory");
+            // (+ the stream prefetches issued after DMA(c+1): two chunks' worth)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kNBuf >= 3 ? (kNBuf - 2) * kDmaPerWave + (kPfS ? 2 : 0) : 0)
+                         : "memory");
             __builtin_amdgcn_s_barrier();
 #ifdef TCSC_STAMPS
             const unsigned long long t0 = stamp();
@@ -577,6 +604,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
             load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
             // DMA(c+2) into the buffer chunk c-1 used
             if (kNBuf >= 3 && !kDmaEarly && dma_wave) dma_next_chunk(dma, dbuf);
+            pf_issue(cur);
             dbuf = dbuf == kNBuf - 1 ? 0 : dbuf + 1;
 #ifdef TCSC_STAMPS
             t2 = stamp();  // waits for the stream load too
@@ -1036,6 +1064,25 @@ int choose_slices(int M, int ncols, int K, long long nnz, int G, size_t ws_bytes
     return best_s;
 }
 
+// Stream prefetch parameters: about four chunks ahead and 1.5 chunks wide
+// (tools/ab.sh sweep, DESIGN.md §4: cfg 4 streams average ~140 B per chunk
+// and take 512 B x 2 lines, cfg 2/3's ~320 B take 4 lines).
+static int env_int(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    return v ? std::atoi(v) : dflt;
+}
+
+void pf_stream_params(long long n_entries, int n_groups, int n_chunks, int* dist, int* lines) {
+    static const int env_dist = env_int("TCSC_PF_DIST", -1), env_lines = env_int("TCSC_PF_LINES", 0);
+    const double per_chunk = n_groups > 0 && n_chunks > 0 ? 8.0 * (double)n_entries / ((double)n_groups * n_chunks) : 0.0;
+    int l = env_lines > 0 ? env_lines : (int)std::ceil(1.5 * per_chunk / 128.0);
+    l = l <= 1 ? 1 : l <= 2 ? 2 : l <= 4 ? 4 : 8;
+    int d = env_dist >= 0 ? env_dist : (int)std::lround(4.0 * per_chunk / 128.0) * 128;
+    d = std::min(std::max(d, 0), kPfWindow - 128 * l) & ~3;
+    *dist = d;
+    *lines = l;
+}
+
 template <bool BF, bool PR>
 static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
     const int nch = (g.K + kTK - 1) / kTK;
@@ -1045,26 +1092,29 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
     const int ldxt = ldxt_of(g.M);
     dim3 grid((g.n_groups + kWaves - 1) / kWaves, (g.M + kTM - 1) / kTM, slices);
     dim3 block(kWaves * 64);
+    int pfd = 0, pfl = 1;
+    pf_stream_params(g.n_entries, g.n_groups, nch, &pfd, &pfl);
     if (g.order == 1) {
         hipLaunchKernelGGL((k_stream<BF, PR, 0, 1>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
                            g.n_entries, g.ent2, g.sptr2, g.n_entries2, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy,
-                           g.a, g.ws);
+                           g.a, g.ws, pfd, pfl);
         return hipGetLastError();
     }
     if (g.order == 2) {
         hipLaunchKernelGGL((k_stream<false, PR, 0, 2>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
                            g.n_entries, g.ent2, g.sptr2, g.n_entries2, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy,
-                           g.a, g.ws);
+                           g.a, g.ws, pfd, pfl);
         return hipGetLastError();
     }
     if (slices == 1) {
         hipLaunchKernelGGL((k_stream<BF, PR, 0, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
                            g.n_entries, g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy,
-                           g.a, g.ws);
+                           g.a, g.ws, pfd, pfl);
         return hipGetLastError();
     }
     hipLaunchKernelGGL((k_stream<BF, PR, 1, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr, g.n_entries,
-                       g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws);
+                       g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws, pfd,
+                       pfl);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const long long total = (long long)g.M * g.ncols;

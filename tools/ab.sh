@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B timing of library builds in one session, alternating (ROUNDS, default 2):
-#   ab.sh name=lib ...        [PARITY=lib: the GPU suite on that build first]
+#   ab.sh name=lib[@VAR=v,VAR2=w] ...   [PARITY=lib: the GPU suite on that build first]
 # Prints k_stream (kernel_ms), the whole step and the other configs' steps.
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
 set -o pipefail
@@ -11,8 +11,9 @@ if [ -n "$PARITY" ]; then
 fi
 for r in $(seq 1 ${ROUNDS:-2}); do
   for spec in "$@"; do
-    n=${spec%%=*}; lib=${spec#*=}
-    TCSC_AMD_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-dense-baseline \
+    n=${spec%%=*}; lib=${spec#*=}; envs=""
+    case "$lib" in *@*) envs=${lib#*@}; lib=${lib%%@*};; esac
+    env ${envs//,/ } TCSC_AMD_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-dense-baseline \
         --no-bcsr --no-host-api --no-graph ${BENCH_ARGS:-} > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err \
         || { echo "$n failed"; tail -5 gpurun_out/ab_$n.err; exit 1; }
     python -c "import json; d=json.load(open('gpurun_out/ab_$n.json')); r=d['roofline']; print('round $r $n k_stream', round(r['kernel_ms'],4), 'step', round(d['ms_per_step'],4), 'T', round(r['transpose_ms'],4), {k: round(v['ms'],4) for k, v in d.get('other_configs',{}).items()}, 'ref', {k: round(v['ms'],3) for k, v in d.get('reference_order',{}).items() if isinstance(v, dict)})"
