@@ -298,7 +298,6 @@ typedef __attribute__((address_space(4))) const i32x16 const_i32x16;
 // a multiple of 16 dwords)
 typedef int sbuf_tail_t __attribute__((ext_vector_type(TCSC_SBUF_TAIL ? TCSC_SBUF_TAIL : 4)));
 typedef __attribute__((address_space(4))) const sbuf_tail_t const_sbuf_tail;
-static_assert(TCSC_GEN_TOUCH == 0, "the chunk loop passes no scalar-cache touch operands");
 
 // Consume this wave's stream for one chunk.  The chunk's header {nb, rem,
 // bytes to the next header, 0} and first TCSC_GEN_CAP entries are already in
@@ -310,8 +309,8 @@ __device__ __forceinline__ void gather_stream(i32x16 (&sb)[TCSC_SBUF_VECS], sbuf
                                               unsigned long long& ptr, unsigned lane, unsigned mask,
                                               facc_t (&acc)[TCSC_ACC_VECS]) {
     (void)sbt;
-#if defined(TCSC_GEN_PF) && TCSC_GEN_PF
-    int junk = 0;  // destination of the reload prefetch (tools/gen_gather_asm.py --pf)
+#if (defined(TCSC_GEN_PF) && TCSC_GEN_PF) || TCSC_GEN_TOUCH
+    int junk = 0;  // destination of the scalar-cache touches (tools/gen_gather_asm.py --touch / --pf)
     asm volatile(TCSC_GATHER_ASM
                  : TCSC_ACC_OPERANDS(acc), TCSC_SBUF_OPERANDS(sb, sbt), TCSC_PTR_OPERAND(ptr), TCSC_JUNK_OPERAND(junk)
                  : [lane] "v"(lane * 16u), [mask] "v"(mask)

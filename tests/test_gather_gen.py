@@ -122,15 +122,18 @@ GEOS = [dict(cw=16, batch=4, cap=24), dict(cw=16, batch=4, cap=16), dict(cw=16, 
         dict(cw=16, batch=2, cap=24)]
 
 
+@pytest.mark.parametrize("touch", [0, 2])
 @pytest.mark.parametrize("pf", [0, 3])
 @pytest.mark.parametrize("depth", [1, 2])
 @pytest.mark.parametrize("geo", GEOS, ids=lambda d: "b{batch}_c{cap}".format(**d))
-def test_tail_loop_gathers_each_entry_once(geo, depth, pf):
+def test_tail_loop_gathers_each_entry_once(geo, depth, pf, touch):
     try:
-        g = gen.Geo(budget=128, depth=depth, touch=0, tail=1, pf=pf, **geo)
+        g = gen.Geo(budget=128, depth=depth, touch=touch, tail=1, pf=pf, **geo)
     except AssertionError as e:
         pytest.skip(f"geometry not valid at this depth: {e}")
     lines = gen.generate_tail(g)
+    if touch or pf:  # the junk SGPR's loads have landed before the loop hands it back
+        assert lines[lines.index(".Lend%=:") + 1] == "s_waitcnt lgkmcnt(0)"
     for n in range(3 * g.cap + 2 * g.batch + 1):
         reads, fmas = simulate(g, lines, n // g.batch, n % g.batch)
         assert sorted(reads) == list(range(n)) and set(reads.values()) <= {1}, n

@@ -54,7 +54,7 @@ import sys
 
 
 class Geo:
-    def __init__(self, cw, batch, cap, budget, depth=1, touch=4, tail=1, hdr=4, pf=0):
+    def __init__(self, cw, batch, cap, budget, depth=1, touch=0, tail=1, hdr=4, pf=0):
         assert cw % 4 == 0 and cap % batch == 0 and 36 + hdr + 2 * cap <= 100
         assert hdr == 4 and (hdr + 2 * cap) % 4 == 0
         assert 1 <= depth and depth * batch <= 15, "lgkmcnt counts to 15"
@@ -164,15 +164,7 @@ def generate(g):
             out += fma(g, q, g.batch * (last - q))
         return out
 
-    L = []
-    # Warm the scalar cache with the next chunk's stream (its start is known
-    # here), so the real s_load after this gather hits in K$ instead of
-    # paying an L2 round trip on the critical path after the barrier.  The
-    # loads land in the junk SGPR (pinned, never read); while they are in
-    # flight the lgkmcnt waits below are conservative, never wrong.
-    for t in range(g.touch):
-        off = min(64 * t, 8 * g.cap - 4)
-        L.append(f"s_load_dword %[junk], %[tptr], {hex(off)}")
+    L = touch(g)
     L += [f"s_cmp_eq_u32 {g.nb}, 0", "s_cbranch_scc1 .Lend%="]
     L.append(".Lphase%=:")
     for p in range(g.npos):
@@ -191,7 +183,19 @@ def generate(g):
         if p != g.npos - 1:
             L.append("s_branch .Lend%=")
     L.append(".Lend%=:")
+    if g.touch:
+        L.append("s_waitcnt lgkmcnt(0)")  # touches still in flight must land before %[junk] is released
     return L + advance(g)
+
+
+def touch(g):
+    """Warm the scalar cache with the NEXT chunk's stream: its header is
+    `next` bytes past this one's (the header's third dword, an SGPR offset
+    of the load), so the real s_load after this gather hits K$ instead of
+    paying an L2 round trip on the critical path after the barrier.  The
+    loads land in the junk SGPR (pinned, never read); while one is in
+    flight a counted LDS wait may wait for one more read, never fewer."""
+    return [f"s_load_dword %[junk], s[{g.ptr}:{g.ptr + 1}], {g.next} offset:{hex(64 * t)}" for t in range(g.touch)]
 
 
 def generate_tail(g):
@@ -204,8 +208,7 @@ def generate_tail(g):
     if ABL == 5:
         return []
     D = g.depth
-    L = ["s_load_dword %[junk], %[tptr], " + hex(min(64 * t, 8 * g.cap - 4)) for t in range(g.touch)]
-    L += prefetch(g)
+    L = touch(g) + prefetch(g)
     L.append(".Lphase%=:")
     for p in range(g.npos):
         L += [f"s_cmp_eq_u32 {g.nb}, {p}", f"s_cbranch_scc1 .Ltail{p}%="]
@@ -232,8 +235,8 @@ def generate_tail(g):
             if not (p == g.npos - 1 and r == 0):
                 L.append("s_branch .Lend%=")
     L.append(".Lend%=:")
-    if g.pf:
-        L.append("s_waitcnt lgkmcnt(0)")  # a prefetch still in flight must land before %[junk] is released
+    if g.pf or g.touch:
+        L.append("s_waitcnt lgkmcnt(0)")  # a touch still in flight must land before %[junk] is released
     return L + advance(g)
 
 
