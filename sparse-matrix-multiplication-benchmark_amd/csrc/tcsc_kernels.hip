@@ -1072,7 +1072,7 @@ static int env_int(const char* name, int dflt) {
 }
 
 void pf_stream_params(long long n_entries, int n_groups, int n_chunks, int* dist, int* lines) {
-    static const int env_dist = env_int("TCSC_PF_DIST", -1), env_lines = env_int("TCSC_PF_LINES", 0);
+    const int env_dist = env_int("TCSC_PF_DIST", -1), env_lines = env_int("TCSC_PF_LINES", 0);  // read per launch
     const double per_chunk = n_groups > 0 && n_chunks > 0 ? 8.0 * (double)n_entries / ((double)n_groups * n_chunks) : 0.0;
     int l = env_lines > 0 ? env_lines : (int)std::ceil(1.5 * per_chunk / 128.0);
     l = l <= 1 ? 1 : l <= 2 ? 2 : l <= 4 ? 4 : 8;

@@ -380,6 +380,36 @@ def test_split_k_paths(gpu, torch_cuda, oracle, monkeypatch, slices):
     plan.destroy()
 
 
+@pytest.mark.parametrize("dist,lines", [("0", "1"), ("1664", "1"), ("768", "8"), ("4000", "8")])
+def test_stream_prefetch_settings_do_not_change_bits(gpu, torch_cuda, oracle, monkeypatch, dist, lines):
+    """The entry-stream L2 prefetch (TCSC_PF_DIST / TCSC_PF_LINES, clamped to
+    the plan's guard window) only touches lines: every setting gives the
+    default's bits.  N = 200 leaves idle waves on the empty chain, whose
+    prefetch window ends in the guard entries; split-K too."""
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    M, K, N = 300, 1500, 200
+    Wd = oracle.ternary((K, N), 0.05, 31)
+    Wm = tcsc_amd.TcscMatrix.from_dense(Wd)
+    X = torch.from_numpy(oracle.uniform((M, K), 32)).to(dev)
+    B = torch.from_numpy(oracle.uniform((N,), 33)).to(dev)
+    for slices in ("1", "3"):
+        monkeypatch.setenv("TCSC_SLICES", slices)
+        plan = tcsc_amd.Plan(Wm)
+        plan.reserve(M)
+        monkeypatch.delenv("TCSC_PF_DIST", raising=False)
+        monkeypatch.delenv("TCSC_PF_LINES", raising=False)
+        Y0 = torch.empty((M, N), device=dev)
+        plan.sgemm(X, B, Y0, M, N, "prelu_basic", 0.2)
+        monkeypatch.setenv("TCSC_PF_DIST", dist)
+        monkeypatch.setenv("TCSC_PF_LINES", lines)
+        Y1 = torch.full((M, N), float("nan"), device=dev)
+        plan.sgemm(X, B, Y1, M, N, "prelu_basic", 0.2)
+        torch.cuda.synchronize()
+        assert torch.equal(Y0.view(torch.int32), Y1.view(torch.int32)), (dist, lines, slices)
+        plan.destroy()
+
+
 @pytest.mark.parametrize("axis,shards,bands", [("cols", 2, 3), ("cols", 3, 4), ("rows", 2, 2)])
 def test_host_bands_with_blocks_bit_identical(gpu, oracle, axis, shards, bands, monkeypatch):
     """The pinned-staging band pipeline under the host API's blocks: column
