@@ -7,7 +7,7 @@
 # tools/traffic_json.py applies the gfx950 x2 FETCH_SIZE correction to the
 # 16-B/lane X^T reads only; it writes profiles/traffic.json for bench.py.
 cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp; mkdir -p gpurun_out
-B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
+B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-api --no-graph ${BENCH_ARGS:-}"
 i=0
 for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))

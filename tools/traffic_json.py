@@ -26,12 +26,20 @@ KERNEL = os.environ.get("TRAFFIC_KERNEL", "k_stream<false, true, 0, 0>")
 
 
 def per_dispatch(root, counter, kernel=KERNEL):
+    """Per-dispatch sums of `counter` over the kernel's full-size launches
+    (the largest grid of the run: bench.py's host-API line launches the same
+    kernel on row bands, which are not the cfg 4 launch)."""
     vals = collections.defaultdict(float)
+    grid = {}
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
-    return list(vals.values())
+                grid[r["Dispatch_Id"]] = int(r["Grid_Size"])
+    if not grid:
+        return []
+    full = max(grid.values())
+    return [v for d, v in vals.items() if grid[d] == full]
 
 
 def main():
@@ -46,19 +54,23 @@ def main():
         return 1
     f_kib = sum(fetch) / len(fetch)
     w_kib = sum(write) / len(write)
-    s_kib = sum(nodma) / len(nodma) if nodma else 0.0  # entry streams (scalar loads)
+    s_kib = sum(nodma) / len(nodma) if nodma else 0.0  # entry streams (no-DMA ablation pass)
     x_kib = f_kib - s_kib                               # X^T through the LDS-DMA (16 B/lane)
+    # Since round 3 the entry streams reach L2 through the stream prefetch's
+    # vector loads (whole 128-B lines, tallied at 64 B like the LDS-DMA's), so
+    # the x2 applies to both parts (an upper bound where a scalar load missed).
     rec = {
         "kernel": KERNEL,
         "fetch_size_kib_raw": f_kib,
         "stream_fetch_kib_raw": s_kib if nodma else None,
         "write_size_kib": w_kib,
         "xt_bytes": 2.0 * x_kib * 1024.0,
-        "stream_bytes": s_kib * 1024.0,
+        "stream_bytes": 2.0 * s_kib * 1024.0,
         "write_bytes": w_kib * 1024.0,
-        "hbm_bytes_per_launch": (2.0 * x_kib + s_kib + w_kib) * 1024.0,
-        "correction": "FETCH_SIZE x2 for the X^T part (gfx950, 16-B/lane streaming reads), the entry-stream "
-                      "part (no-DMA ablation pass) and WRITE_SIZE as counted",
+        "hbm_bytes_per_launch": (2.0 * x_kib + 2.0 * s_kib + w_kib) * 1024.0,
+        "correction": "FETCH_SIZE x2 (gfx950: 128-B line requests tallied at 64 B) for the X^T part (LDS-DMA, "
+                      "16 B/lane) and the entry-stream part (no-DMA ablation pass; L2-filled by the stream "
+                      "prefetch's vector loads), WRITE_SIZE as counted; full-size launches only",
         "l2_hit_rate": (sum(hit) / (sum(hit) + sum(miss))) if hit and miss else None,
         "dispatches": [len(fetch), len(write), len(nodma)],
     }
