@@ -25,7 +25,9 @@
 //    stream with s_load_dwordx16 (8 entries per scalar load) and selects the
 //    accumulator of the entry's column with s_set_gpr_idx_on (relative VGPR
 //    addressing on the v_pk_fma DST/SRC2): no per-column loop, no branch per
-//    nonzero, 2 SALU + 3 VALU + 1 LDS instruction per nonzero.
+//    nonzero, 2 SALU + 3 VALU + 1 LDS instruction per nonzero.  Each wave
+//    also pulls its stream ~4 chunks ahead into L2 (one LDS-DMA dword load
+//    per chunk into a scratch), so the next chunk's scalar load hits L2.
 //  * Accumulators (4*kCW VGPRs) live in registers for the whole K range; the
 //    epilogue adds the bias (first or last, matching the reference variant's
 //    order) and applies PReLU before the only store of Y.  Small grids split
