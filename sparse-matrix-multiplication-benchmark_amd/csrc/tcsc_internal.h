@@ -100,15 +100,19 @@ constexpr int kEpiMinBytes = kWaves * 64 * (kCW * 4 + 16);
 constexpr int kLdsBytes = (kRingBytes + kPfScratch) > kEpiMinBytes ? (kRingBytes + kPfScratch) : kEpiMinBytes;
 // Staging: waves 0..kDmaWaves-1 move a chunk, kDmaPerWave 1-KiB rows each,
 // right after the chunk loop's barrier (TCSC_DMA_EARLY=1) or after their
-// gather (0).  Default: the first half of the waves.  The SIMD arbiter
-// favours older waves (tools/trace.py: waves 0-3 finish their gathers first,
-// 12-15 last), so the DMA issue (~100 cycles per row) lands on waves with
-// slack at the barrier instead of on the critical path (A/B: -2.5 %).
+// gather (0).  The SIMD arbiter favours older waves (tools/trace.py: waves
+// 0-3 finish their gathers first, 12-15 last), so the DMA issue (~100 cycles
+// per row) goes to the oldest waves, which have slack at the barrier.
+// Round 1 measured the first half of the waves, issuing after the gather,
+// 2.5 % faster than all 16.  Since round 3's stream prefetch, the DMA is issued
+// by the first 4 waves, early: DMA(c+2) starts right after chunk c's barrier
+// and so gets one more gather of lead time (tools/ab.sh, 3 rounds alternating:
+// k_stream 1.160-1.162 -> 1.145-1.148 ms, step 1.245-1.253 -> 1.222-1.236 ms).
 #ifndef TCSC_DMA_WAVES
-#define TCSC_DMA_WAVES (TCSC_WAVES / 2)
+#define TCSC_DMA_WAVES (TCSC_WAVES / 4)
 #endif
 #ifndef TCSC_DMA_EARLY
-#define TCSC_DMA_EARLY 0
+#define TCSC_DMA_EARLY 1
 #endif
 constexpr int kDmaWaves = TCSC_DMA_WAVES;
 constexpr bool kDmaEarly = TCSC_DMA_EARLY != 0;
