@@ -338,7 +338,7 @@ def main():
             # launch gaps between k_transpose and k_stream cost on the eager stream
             out["graph"] = graph_line(plan, X, B, Y, cfg.M, ncols, variant, args.steps, stream, elapsed_max)
         if world == 1 and not args.no_other_configs and not args.override:
-            out["other_configs"] = other_configs(tcsc_amd, workloads, dev, sh, timed, cfg.idx)
+            out["other_configs"] = other_configs(args, tcsc_amd, workloads, dev, sh, timed, cfg.idx)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, cfg, variant, X, B, csp, csn, rip[:npos], rin[:nneg])
         print(json.dumps(out), flush=True)
@@ -434,15 +434,21 @@ def host_api_line(tcsc_amd, cfg, ncols, variant, X, B, Y, csp, csn, rip, rin, ad
             "note": "pageable host X/B/Y; H2D + kernels + D2H, row bands through pinned slots over 3 streams"}
 
 
-def other_configs(tcsc_amd, workloads, dev, sh, timed, skip):
+MFMA_BF16_PEAK = 2.5e15  # dense bf16 MFMA FLOP/s (MI355X_MICROARCH.md chip table, spec)
+
+
+def other_configs(args, tcsc_amd, workloads, dev, sh, timed, skip):
     """The other BASELINE configs on this GPU (not part of `value`): one full
     tcsc_gpu_sgemm per step (X staging + gather, or split + GEMM on the MFMA
     path for near-dense W), inputs resident, HIP events over 30 launches
-    after 10 warm-up launches."""
+    after 10 warm-up launches; each with the roof that binds it (LDS gather
+    for the gather path, bf16 MFMA for the MFMA path) and, unless
+    --no-cpu-baseline, the reference's CPU path timed beside it (SURVEY.md
+    §8d: main.cpp's own loop for cfg 1-3, 1 warm-up + median of 3 for cfg 5)."""
     import torch
 
     res = {}
-    for idx in (2, 3, 5):
+    for idx in (1, 2, 3, 5):
         if idx == skip:
             continue
         c = workloads.CONFIGS[idx]
@@ -456,7 +462,8 @@ def other_configs(tcsc_amd, workloads, dev, sh, timed, skip):
         del inp["Wd"]
         plan = tcsc_amd.Plan.from_device(c.K, c.N, csp, csn, rip, rin, 0, c.N, dev.index or 0, sh)
         plan.reserve(c.M)
-        mfma_min = plan.info()["mfma_min_M"]
+        info = plan.info()
+        mfma_min = info["mfma_min_M"]
         Yc = torch.empty((c.M, c.N), device=dev)
 
         def one():
@@ -466,12 +473,28 @@ def other_configs(tcsc_amd, workloads, dev, sh, timed, skip):
             one()
         t = timed(one, 30)
         nnz = npos + nneg
-        res[c.name] = {
+        mfma = bool(mfma_min and c.M >= mfma_min)
+        path = ("mfma (bf16 x3 split GEMM)" if mfma else
+                "small-M (one wave per column)" if c.M <= 16 else "gather (k_stream)")
+        r = {
             "workload": c.describe(), "variant": c.variant, "nnz": nnz, "ms": t * 1e3,
             "g_add_ops_per_s": workloads.add_ops(c.M, nnz, c.N) / t / 1e9,
             "hbm_frac": workloads.algorithmic_bytes(c.M, c.K, c.N, nnz) / t / (HBM_PEAK_GBS * 1e9),
-            "path": "mfma (bf16 x3 split GEMM)" if mfma_min and c.M >= mfma_min else "gather (k_stream)",
+            "path": path,
         }
+        if mfma:
+            ldk = (3 * c.K + 63) // 64 * 64  # the split GEMM's depth (tcsc_internal.h mfma_ldk)
+            flops = 2.0 * c.M * c.N * ldk
+            r["mfma_flops_per_step"] = flops
+            r["mfma_frac"] = flops / t / MFMA_BF16_PEAK
+        else:
+            r["lds_gather_frac"] = (c.M * nnz / t) / LDS_GATHER_PEAK
+        if not args.no_cpu_baseline:
+            cb = cpu_baseline(args, c, c.variant, inp["X"], inp["B"], csp, csn, rip[:npos], rin[:nneg],
+                              protocol="harness" if idx <= 3 else "median3", seconds=8.0, legs=False)
+            r["cpu_baseline"] = cb
+            r["gpu_vs_cpu_1core"] = r["g_add_ops_per_s"] / cb["value"]
+        res[c.name] = r
         plan.destroy()
         del inp, csp, csn, rip, rin, Yc
     torch.cuda.empty_cache()
@@ -606,18 +629,53 @@ def usable_cpus():
     return (min(n_aff, quota) if quota else n_aff), {"nproc": n_host, "affinity": n_aff, "cgroup_quota_cpus": quota}
 
 
-def cpu_baseline(args, cfg, variant, X, B, csp, csn, rip, rin):
+# main.cpp:9-17: NUM_RUNS 20, CYCLES_REQUIRED 1e8 (TSC cycles), REP 50.  The
+# harness's cycle counter ticks at the TSC rate (~2 GHz on these hosts), so
+# 1e8 cycles is taken as 0.05 s of wall time.
+NUM_RUNS, REP, CYCLES_REQUIRED_S = 20, 50, 0.05
+
+
+def harness_protocol(call):
+    """measure_tcsc_cycles (main.cpp:54-113) around a zero-argument call:
+    warm-up passes of num_runs calls, num_runs scaled by CYCLES_REQUIRED /
+    cycles until the multiplier is <= 2, then REP passes of num_runs calls;
+    returns (mean seconds per call over the REP passes, num_runs)."""
+    num_runs, multiplier = NUM_RUNS, 1.0
+    while True:
+        num_runs = max(1, int(num_runs * multiplier))
+        t0 = time.perf_counter()
+        for _ in range(num_runs):
+            call()
+        multiplier = CYCLES_REQUIRED_S / max(time.perf_counter() - t0, 1e-9)
+        if multiplier <= 2:
+            break
+    total = 0.0
+    for _ in range(REP):
+        t0 = time.perf_counter()
+        for _ in range(num_runs):
+            call()
+        total += (time.perf_counter() - t0) / num_runs
+    return total / REP, num_runs
+
+
+def cpu_baseline(args, cfg, variant, X, B, csp, csn, rip, rin, protocol="median3", seconds=None, legs=True):
     """SURVEY.md §8d, on this GPU box's host, rank 0 at N=1, on row samples
     of the same workload (all columns):
       * value: the reference's own tcsc_sgemm_<variant> (sparse/tcsc.c
         compiled in place with its authors' flags, -O3 -ffast-math, AVX2+FMA:
         oracle/_ref/libtcsc_ref_fast.so) on 1 core, as benchmark.sh pins it
-        (benchmark.sh:36): 1 warm-up pass, then the median of 3 passes;
-      * the same sources built IEEE (-O2, no fast-math: the parity build) and
-        the oracle's C restatement, each 1 core, median of 3;
-      * the reference's own OpenMP sparseGEMM_PReLU (SparseGEMM.h:151-168,
-        the multi-core form it ships) on every usable core, median of 3 over
-        all M rows.
+        (benchmark.sh:36), timed with
+          protocol "harness": the harness's own loop (main.cpp:54-113: warm-up
+            until a pass covers CYCLES_REQUIRED, then REP passes of num_runs
+            calls, the mean per call) on a row sample sized so one call takes
+            a few ms (cfg 1-3);
+          protocol "median3": 1 warm-up pass over the sample, then the median
+            of 3 passes (cfg 4-5, where one harness run would take hours);
+      * (legs=True) the same sources built IEEE (-O2, no fast-math: the parity
+        build) and the oracle's C restatement, each 1 core, median of 3;
+      * the reference's own OpenMP sparseGEMM_PReLU / sparseGEMM
+        (SparseGEMM.h:104-168, the multi-core form it ships) on every usable
+        core, median of 3 (all M rows, or a row sample of about 1 s per pass).
     Falls back to the oracle restatement ("port") where oracle/_ref is absent."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
@@ -626,59 +684,85 @@ def cpu_baseline(args, cfg, variant, X, B, csp, csn, rip, rin):
 
     o = pyoracle.load_oracle()
     ref_fast = pyoracle.load_reference(fast=True)
-    ref_ieee = pyoracle.load_reference()
+    ref_ieee = pyoracle.load_reference() if legs else None
     ncols = csp.numel() - 1
     W = pyoracle.TCSC(cfg.K, ncols, csp.cpu().numpy(), csn.cpu().numpy(), rip.cpu().numpy(), rin.cpu().numpy())
     Bh = B.cpu().numpy()
     Xh = X.cpu().numpy()
     nnz = W.nnz
     var = variant if variant in pyoracle.VARIANTS else "prelu_basic"
+    seconds = args.cpu_seconds if seconds is None else seconds
 
     def rate(rows, t):
         return (rows * nnz + rows * ncols) / t / 1e9
 
-    def one_core(fn, seconds):
-        """1 warm-up pass on 8 rows sizes the sample so that one pass takes
-        about `seconds`; then the median of 3 timed passes over it."""
+    def probe(fn):
+        """seconds per row of one call, from an 8-row probe call (sizes the sample only)"""
+        n = min(8, cfg.M)
+        fn(var, Xh[:n], W, Bh, 0.2)  # first touch of W and the code
         t0 = time.perf_counter()
-        fn(var, Xh[:8], W, Bh, 0.2)
-        per_row = (time.perf_counter() - t0) / 8
-        rows = int(min(cfg.M, max(8, seconds / max(per_row, 1e-9))))
+        fn(var, Xh[:n], W, Bh, 0.2)
+        return (time.perf_counter() - t0) / n
+
+    def median3(fn, secs):
+        """1 warm-up pass over the sample, then the median of 3 timed passes
+        over it; the sample is sized so that one pass takes about `secs`."""
+        rows = int(min(cfg.M, max(8, secs / max(probe(fn), 1e-9))))
+        fn(var, Xh[:rows], W, Bh, 0.2)  # warm-up pass
         ts = []
         for _ in range(3):
             t0 = time.perf_counter()
             fn(var, Xh[:rows], W, Bh, 0.2)
             ts.append(time.perf_counter() - t0)
         t = float(np.median(ts))
-        return {"rows": rows, "median_s": t, "value": rate(rows, t)}
+        return {"rows": rows, "median_s": t, "value": rate(rows, t), "protocol": "1 warm-up pass + median of 3"}
 
-    budget = args.cpu_seconds
-    legs = {}
+    def harness(lib):
+        """main.cpp's loop on a row sample of ~2.5 ms per call"""
+        rows = int(min(cfg.M, max(1, 2.5e-3 / max(probe(lib.sgemm), 1e-9))))
+        call = lib.sgemm_call(var, Xh[:rows], W, Bh, 0.2)
+        t, runs = harness_protocol(call)
+        return {"rows": rows, "mean_call_s": t, "num_runs": runs, "rep": REP, "value": rate(rows, t),
+                "protocol": f"main.cpp:54-113 loop (NUM_RUNS {NUM_RUNS} scaled to >= {CYCLES_REQUIRED_S} s "
+                            f"per pass -> {runs}, REP {REP}, mean per call)"}
+
+    out_legs = {}
     if ref_fast:
-        legs["reference_fast"] = one_core(ref_fast.sgemm, budget * 0.14)
+        out_legs["reference_fast"] = harness(ref_fast) if protocol == "harness" else median3(ref_fast.sgemm,
+                                                                                            seconds * 0.12)
     if ref_ieee:
-        legs["reference_ieee"] = one_core(ref_ieee.sgemm, budget * 0.07)
-    legs["port"] = one_core(o.sgemm, budget * 0.07)
+        out_legs["reference_ieee"] = median3(ref_ieee.sgemm, seconds * 0.05)
+    if legs or not ref_fast:
+        out_legs["port"] = median3(o.sgemm, seconds * 0.05)
     threads, cpu_info = usable_cpus()
     omp_env = os.environ.get("OMP_NUM_THREADS")
     if omp_env:
         threads = min(threads, int(omp_env)) if omp_env.isdigit() else threads
     omp_lib = ref_fast or ref_ieee
+    prelu = var in pyoracle.PRELU_VARIANTS
+    # all rows unless a pass would take much longer than ~1 s (cfg 5)
+    omp_rows = cfg.M
+    per_row_1core = 1.0 / (out_legs.get("reference_fast") or out_legs["port"])["value"] * (nnz + ncols) / 1e9
+    if per_row_1core * cfg.M / max(threads, 1) > 1.0:
+        omp_rows = int(max(threads, min(cfg.M, 1.0 * threads / per_row_1core)))
     ts = []
-    for _ in range(3):
+    for i in range(4):  # the first pass starts the thread team (not timed)
         t0 = time.perf_counter()
         if omp_lib:
             o.set_omp_threads(threads)
-            omp_lib.sparse_gemm(Xh, W, Bh, prelu=True, a=0.2)
+            omp_lib.sparse_gemm(Xh[:omp_rows], W, Bh, prelu=prelu, a=0.2)
         else:
-            o.sparse_gemm_omp(Xh, W, Bh, prelu=True, a=0.2, threads=threads)
-        ts.append(time.perf_counter() - t0)
+            o.sparse_gemm_omp(Xh[:omp_rows], W, Bh, prelu=prelu, a=0.2, threads=threads)
+        if i:
+            ts.append(time.perf_counter() - t0)
     t_omp = float(np.median(ts))
-    main = legs.get("reference_fast") or legs.get("reference_ieee") or legs["port"]
+    main = out_legs.get("reference_fast") or out_legs.get("reference_ieee") or out_legs["port"]
     kind = "reference" if (ref_fast or ref_ieee) else "port"
     flags = ("g++ -O3 -ffast-math -mavx2 -mfma (the reference's build_and_run_m1.sh:77 flags, "
              "-march=native pinned to AVX2+FMA)" if ref_fast else
              "g++ -O2 -fno-fast-math -ffp-contract=off (IEEE parity build)" if ref_ieee else "gcc -O2")
+    how = (f"{main['protocol']} ({main['mean_call_s'] * 1e3:.2f} ms per call)" if "mean_call_s" in main else
+           f"{main['protocol']} passes ({main['median_s']:.2f} s each)")
     out = {
         "value": main["value"],
         "unit": "G-add-ops/s",
@@ -686,14 +770,16 @@ def cpu_baseline(args, cfg, variant, X, B, csp, csn, rip, rin):
         "kind": kind,
         "sample": (f"{cfg.name}: first {main['rows']} of {cfg.M} rows x all {ncols} columns, tcsc_sgemm_{var}, "
                    f"{'sparse/tcsc.c compiled in place' if kind == 'reference' else 'oracle/tcsc_oracle.c'} "
-                   f"({flags}), 1 core, 1 warm-up + median of 3 passes ({main['median_s']:.2f} s each)"),
+                   f"({flags}), 1 core, {how}"),
         "flags": flags,
-        "legs": legs,
-        "omp_value": rate(cfg.M, t_omp),
+        "legs": out_legs,
+        "omp_value": rate(omp_rows, t_omp),
         "omp_cores": threads,
-        "omp_kind": "reference sparseGEMM_PReLU (SparseGEMM.h:151-168, OpenMP)" if omp_lib else
+        "omp_cores_of_host": f"{threads} of {cpu_info['nproc']} host CPUs (affinity/cgroup share)",
+        "omp_kind": (f"reference sparseGEMM{'_PReLU' if prelu else ''} (SparseGEMM.h:"
+                     f"{'151-168' if prelu else '104-119'}, OpenMP)") if omp_lib else
                     "oracle_sparse_gemm_omp restatement",
-        "omp_sample": f"all {cfg.M} rows x {ncols} columns, median of 3 ({t_omp:.2f} s each)",
+        "omp_sample": f"first {omp_rows} of {cfg.M} rows x {ncols} columns, 1 warm-up + median of 3 ({t_omp:.3g} s each)",
         "host_cpus": cpu_info,
     }
     return out

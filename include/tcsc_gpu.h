@@ -163,7 +163,11 @@ int tcsc_gpu_sgemm_prepared(const tcsc_gpu_plan *plan, const float *dB, float *d
  * device -> TCSC arrays on the device, bit-exact with the reference builder
  * (tcsc.c:6-66).  Two calls: first with the four output pointers NULL to
  * get n_pos / n_neg (col_start arrays are still written), then with the
- * index arrays allocated.  Synchronises `stream`. */
+ * index arrays allocated.  The matrix must not change between the two calls
+ * of a pair (the second call reuses the first call's per-tile counts when it
+ * follows it directly with the same matrix, shape and col_start arrays; the
+ * index arrays are never written past the counted sizes either way).
+ * Synchronises `stream`. */
 int tcsc_gpu_from_dense(const float *d_dense, int rows, int cols,
                         int *d_col_start_pos, int *d_col_start_neg,
                         int *d_row_index_pos, int *d_row_index_neg,
@@ -195,18 +199,6 @@ void tcsc_gpu_cache_clear(void);
  * exercised on a single GPU). 0 restores the default. */
 int tcsc_gpu_num_shards(void);
 void tcsc_gpu_set_num_shards(int shards);
-
-/* Host-side self-test hooks (no GPU needed; tests/test_sanitizers.py runs
- * them in AddressSanitizer / ThreadSanitizer builds of the host code):
- *   tcsc_selftest_fingerprint: the host API's plan-cache fingerprint of W
- *     summed on its worker pool (the path host_sgemm overlaps with a call)
- *     against the same hash summed serially; returns 0 when they agree.
- *   tcsc_selftest_copy2d: `rows` rows of `row_bytes` from src (pitch sp)
- *     to dst (pitch dp) on device `dev`'s copy pool for direction `side`
- *     (0 in, 1 out) -- the pinned-staging copies of the band pipeline. */
-int tcsc_selftest_fingerprint(const tcsc_t *W);
-int tcsc_selftest_copy2d(void *dst, size_t dp, const void *src, size_t sp,
-                         size_t row_bytes, size_t rows, int dev, int side);
 
 #ifdef __cplusplus
 }

@@ -337,6 +337,24 @@ class Reference:
                                 M, W.cols, K)
         return Y
 
+    def sgemm_call(self, variant: str, X, W: TCSC, B, a: float = 0.2):
+        """A zero-argument callable running the reference's tcsc_sgemm_<variant>
+        on fixed arrays (copied once here, not per call): what bench.py's CPU
+        baseline times with the harness's own call loop (main.cpp:54-113)."""
+        X = np.ascontiguousarray(X, np.float32).copy()
+        M, K = X.shape
+        Y = np.empty((M, W.cols), np.float32)
+        keep = (X, W.col_start_pos.copy(), W.col_start_neg.copy(), _nz(W.row_index_pos.copy()),
+                _nz(W.row_index_neg.copy()), _nz(np.ascontiguousarray(B, np.float32).copy()), Y)
+        fn, vid, N = self.lib.ref_tcsc_sgemm, VARIANTS.index(variant), W.cols
+        xv, yv = _nz(keep[0].reshape(-1)), _nz(Y.reshape(-1))
+
+        def call():
+            fn(vid, xv, keep[1], keep[2], keep[3], keep[4], keep[5], a, yv, M, N, K)
+
+        call.keep = keep
+        return call
+
     def gemm_basic(self, X, Wd, B) -> np.ndarray:
         X = np.ascontiguousarray(X, np.float32)
         M, K = X.shape

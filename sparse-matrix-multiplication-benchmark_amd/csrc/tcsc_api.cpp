@@ -565,8 +565,11 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
     // axis (<= 65536 blocks) and 32-bit per-lane DMA offsets within a chunk
     // (kTK rows of ldxt floats): at most 2^22 rows per launch.  A whole call
     // (stage 0) runs as launches of 2^22 rows (whole row tiles) on the same
-    // workspace; the reference accepts any int M (tcsc.c:69).  Each row is
-    // summed as by one launch (M > 2^22 always takes 1 K-slice).
+    // workspace; the reference accepts any int M (tcsc.c:69).  Every
+    // sub-launch runs one K-slice (unless the caller forces a split), so a
+    // ragged last launch sums its rows in the same order as the full ones
+    // (the workspace is sized for all of M, which would otherwise let the
+    // cost model split K for a small tail: ADVICE r3).
     constexpr int kMaxLaunchRows = 1 << 22;
     if (M > kMaxLaunchRows) {
         if (stage != 0) {
@@ -576,7 +579,7 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
         for (int r0 = 0; r0 < M; r0 += kMaxLaunchRows) {
             const int r = std::min(kMaxLaunchRows, M - r0);
             const int rc = sgemm_ws(p, dX + (size_t)r0 * p->rows, dB, dY + (size_t)r0 * ldy, r, ldy, variant, a,
-                                    stream, ws, ws_bytes, 0, force_slices);
+                                    stream, ws, ws_bytes, 0, force_slices > 0 ? force_slices : 1);
             if (rc != TCSC_OK) return rc;
         }
         return TCSC_OK;
@@ -856,13 +859,17 @@ int tcsc_gpu_sgemm_prepared(const tcsc_gpu_plan* p, const float* dB, float* dY, 
 }
 
 // The two calls (counts, then fill) share the tile offsets: the first call
-// keeps them per device, keyed by (matrix, shape), and a second call on the
-// same key fills from them instead of counting again (cfg 4: two reads of
-// the 1-GiB matrix in all instead of three).  The fill writes at most the
-// counted entries, so index arrays sized from the first call are never
-// overrun even if the matrix changed in between.
+// keeps them per device, keyed by (matrix, shape, col_start arrays), and the
+// very next call on the same key fills from them instead of counting again
+// (cfg 4: two reads of the 1-GiB matrix in all instead of three).  Any other
+// call in between drops the kept counts (the next call counts afresh), and
+// include/tcsc_gpu.h requires the matrix to stay unchanged between the two
+// calls of a pair.  The fill writes at most the counted entries, so index
+// arrays sized from the first call are never overrun even if it did change.
 struct DenseBuildScratch {
     const float* key = nullptr;
+    const int* key_csp = nullptr;
+    const int* key_csn = nullptr;
     int rows = -1, cols = -1;
     bool counted = false;
     DevBuf cp, cn, totp, totn, tmp;
@@ -886,7 +893,8 @@ int tcsc_gpu_from_dense(const float* d_dense, int rows, int cols, int* d_csp, in
     const int tr = tcsc::dense_tile_rows(rows), nt = rows > 0 ? (rows + tr - 1) / tr : 0;
     const size_t tile_b = std::max<size_t>(1, (size_t)nt * cols) * sizeof(int);
     const size_t col_b = (size_t)(cols + 1) * sizeof(int);
-    const bool reuse = sc.counted && sc.key == d_dense && sc.rows == rows && sc.cols == cols && d_rip && d_rin;
+    const bool reuse = sc.counted && sc.key == d_dense && sc.key_csp == d_csp && sc.key_csn == d_csn &&
+                       sc.rows == rows && sc.cols == cols && d_rip && d_rin;
     if (!reuse) {
         auto grow = [](DevBuf& b, size_t& cap, size_t want) -> hipError_t {
             if (cap >= want && b.p) return hipSuccess;
@@ -909,6 +917,8 @@ int tcsc_gpu_from_dense(const float* d_dense, int rows, int cols, int* d_csp, in
         HIP_TRY(tcsc::dense_to_tcsc_counts(d_dense, rows, cols, sc.cp.as<int>(), sc.cn.as<int>(), sc.totp.as<int>(),
                                            sc.totn.as<int>(), st));
         sc.key = d_dense;
+        sc.key_csp = d_csp;
+        sc.key_csn = d_csn;
         sc.rows = rows;
         sc.cols = cols;
         sc.counted = true;
@@ -1884,7 +1894,10 @@ void tcsc_dense_gemm_prelu(const float* X, const float* W, const float* b, float
 
 }  // extern "C"
 
-// Self-test hooks (include/tcsc_gpu.h): the worker pools without a GPU.
+// Self-test hooks (tests/native/tcsc_selftest.h): the worker pools without
+// a GPU.  Compiled only into the sanitizer builds (-DTCSC_SELFTEST), never
+// exported by the product library.
+#ifdef TCSC_SELFTEST
 extern "C" {
 
 int tcsc_selftest_fingerprint(const tcsc_t* W) {
@@ -1902,3 +1915,4 @@ int tcsc_selftest_copy2d(void* dst, size_t dp, const void* src, size_t sp, size_
 }
 
 }  // extern "C"
+#endif  // TCSC_SELFTEST

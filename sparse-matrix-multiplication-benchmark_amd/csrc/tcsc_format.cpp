@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <system_error>
 #include <thread>
 #include <vector>
 #include <sched.h>
@@ -265,8 +266,10 @@ bool compare(const dense_t result, const dense_t target, int rows, int cols) {
 // and a rounded add (no contraction), so the bits equal the reference's IEEE
 // build.  Loop order m, k, n (a row of accumulators) instead of m, n, k:
 // each element still sees the same sequence of operations, but W is read
-// along its rows, and row blocks run on the usable CPUs (the reference's
-// harness calls it >= 1,000 times per case at M = 256, main.cpp:376).
+// along its rows.  Single-threaded by default, as the reference's (a
+// harness that times it as its "GEMM" line, main.cpp:379-391, then compares
+// against the same baseline); $TCSC_DENSE_THREADS=n runs row blocks on n
+// threads (0 = the usable CPUs, at most 16), same bits.
 namespace {
 void gemm_rows(const float* X, const float* W, const float* B, float* Y, int m0, int m1, int N, int K) {
 #pragma clang fp contract(off)
@@ -291,12 +294,16 @@ void gemm_rows(const float* X, const float* W, const float* B, float* Y, int m0,
     }
 }
 int gemm_threads(int M, int N, int K) {
+    const char* env = std::getenv("TCSC_DENSE_THREADS");
+    const int want = env ? std::atoi(env) : 1;
+    if (want == 1) return 1;
     cpu_set_t set;
     CPU_ZERO(&set);
     int cpus = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : 1;
     // a thread per >= 4 M multiply-adds of work, at most 16 and one per row
     const double work = (double)M * N * K;
-    return std::max(1, std::min({cpus, 16, M, (int)(work / 4e6) + 1}));
+    const int cap = want > 1 ? want : std::min(cpus, 16);
+    return std::max(1, std::min({cap, M, (int)(work / 4e6) + 1}));
 }
 }  // namespace
 
@@ -308,8 +315,16 @@ void gemm_basic(const dense_t X, const dense_t W, const dense_t B, dense_t Y, in
         return;
     }
     std::vector<std::thread> th;
-    for (int t = 0; t < T; ++t)
-        th.emplace_back(gemm_rows, X, W, B, Y, (int)((long long)M * t / T), (int)((long long)M * (t + 1) / T), N, K);
+    int done = 0;  // rows [0, done) are handed to threads
+    try {
+        for (int t = 0; t < T; ++t) {
+            const int r1 = (int)((long long)M * (t + 1) / T);
+            th.emplace_back(gemm_rows, X, W, B, Y, done, r1, N, K);
+            done = r1;
+        }
+    } catch (const std::system_error&) {  // no thread available: the rest on this one
+    }
+    if (done < M) gemm_rows(X, W, B, Y, done, M, N, K);
     for (auto& x : th) x.join();
 }
 

@@ -313,13 +313,16 @@ __device__ __forceinline__ void gather_stream(i32x16 (&sb)[TCSC_SBUF_VECS], sbuf
     (void)sbt;
 #if (defined(TCSC_GEN_PF) && TCSC_GEN_PF) || TCSC_GEN_TOUCH
     int junk = 0;  // destination of the scalar-cache touches (tools/gen_gather_asm.py --touch / --pf)
+    unsigned m0sv;
     asm volatile(TCSC_GATHER_ASM
-                 : TCSC_ACC_OPERANDS(acc), TCSC_SBUF_OPERANDS(sb, sbt), TCSC_PTR_OPERAND(ptr), TCSC_JUNK_OPERAND(junk)
+                 : TCSC_ACC_OPERANDS(acc), TCSC_SBUF_OPERANDS(sb, sbt), TCSC_PTR_OPERAND(ptr), TCSC_JUNK_OPERAND(junk),
+                   [m0sv] "=&s"(m0sv)
                  : [lane] "v"(lane * 16u), [mask] "v"(mask)
                  : TCSC_GATHER_CLOBBERS);
 #else
+    unsigned m0sv;
     asm volatile(TCSC_GATHER_ASM
-                 : TCSC_ACC_OPERANDS(acc), TCSC_SBUF_OPERANDS(sb, sbt), TCSC_PTR_OPERAND(ptr)
+                 : TCSC_ACC_OPERANDS(acc), TCSC_SBUF_OPERANDS(sb, sbt), TCSC_PTR_OPERAND(ptr), [m0sv] "=&s"(m0sv)
                  : [lane] "v"(lane * 16u), [mask] "v"(mask)
                  : TCSC_GATHER_CLOBBERS);
 #endif
@@ -365,28 +368,31 @@ struct DmaState {
 // ~1.7 (A/B: -0.9 % k_stream at cfg4).  0 = one M0 write per row.
 template <int N>
 __device__ __forceinline__ void dma_rows(unsigned m0, const unsigned* v, const char* src) {
+    unsigned sv;  // M0 is saved and restored around every statement that writes it
     if constexpr (N == 4)
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %5\n\t"
-                     "global_load_lds_dwordx4 %2, %5 offset:1024\n\tglobal_load_lds_dwordx4 %3, %5 offset:2048\n\t"
-                     "global_load_lds_dwordx4 %4, %5 offset:3072"
-                     :
+        asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %6\n\t"
+                     "global_load_lds_dwordx4 %3, %6 offset:1024\n\tglobal_load_lds_dwordx4 %4, %6 offset:2048\n\t"
+                     "global_load_lds_dwordx4 %5, %6 offset:3072\n\ts_mov_b32 m0, %[sv]"
+                     : [sv] "=&s"(sv)
                      : "s"(m0), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "s"(src)
                      : "memory");
     else if constexpr (N == 3)
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %4\n\t"
-                     "global_load_lds_dwordx4 %2, %4 offset:1024\n\tglobal_load_lds_dwordx4 %3, %4 offset:2048"
-                     :
+        asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %5\n\t"
+                     "global_load_lds_dwordx4 %3, %5 offset:1024\n\tglobal_load_lds_dwordx4 %4, %5 offset:2048\n\t"
+                     "s_mov_b32 m0, %[sv]"
+                     : [sv] "=&s"(sv)
                      : "s"(m0), "v"(v[0]), "v"(v[1]), "v"(v[2]), "s"(src)
                      : "memory");
     else if constexpr (N == 2)
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\t"
-                     "global_load_lds_dwordx4 %2, %3 offset:1024"
-                     :
+        asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %4\n\t"
+                     "global_load_lds_dwordx4 %3, %4 offset:1024\n\ts_mov_b32 m0, %[sv]"
+                     : [sv] "=&s"(sv)
                      : "s"(m0), "v"(v[0]), "v"(v[1]), "s"(src)
                      : "memory");
     else
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
-                     :
+        asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3\n\t"
+                     "s_mov_b32 m0, %[sv]"
+                     : [sv] "=&s"(sv)
                      : "s"(m0), "v"(v[0]), "s"(src)
                      : "memory");
 }
@@ -407,11 +413,14 @@ __device__ __forceinline__ void dma_next_chunk(DmaState& d, int buf) {
     dma_groups<0>(d, m0base);
 #else
 #pragma unroll
-    for (int i = 0; i < kDmaPerWave; ++i)
-        asm volatile("s_add_u32 m0, %0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3"
-                     :
+    for (int i = 0; i < kDmaPerWave; ++i) {
+        unsigned sv;
+        asm volatile("s_mov_b32 %[sv], m0\n\ts_add_u32 m0, %1, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %4\n\t"
+                     "s_mov_b32 m0, %[sv]"
+                     : [sv] "=&s"(sv)
                      : "s"(m0base), "n"(i * kRowBytes), "v"(d.voff[i]), "s"(d.next)
                      : "memory", "scc");
+    }
 #endif
 #endif
     d.next += d.chunk_bytes;
@@ -420,7 +429,11 @@ __device__ __forceinline__ void dma_next_chunk(DmaState& d, int buf) {
 // L2 prefetch of the entry stream (kPfS): one global_load_lds_dword per wave
 // and chunk into the wave's 256-B scratch; the data is never read.
 __device__ __forceinline__ void pf_touch(unsigned m0, unsigned voff, const char* base) {
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2" : : "s"(m0), "v"(voff), "s"(base)
+    unsigned sv;
+    asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %2, %3\n\t"
+                 "s_mov_b32 m0, %[sv]"
+                 : [sv] "=&s"(sv)
+                 : "s"(m0), "v"(voff), "s"(base)
                  : "memory");
 }
 

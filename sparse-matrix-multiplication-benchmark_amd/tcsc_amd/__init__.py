@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_gpu_plan_reserve", "tcsc_gpu_plan_destroy", "tcsc_gpu_sgemm", "tcsc_gpu_prepare_x",
     "tcsc_gpu_sgemm_prepared", "tcsc_gpu_from_dense", "tcsc_gpu_dense_sgemm", "tcsc_gpu_last_error",
     "tcsc_gpu_cache_clear", "tcsc_gpu_num_shards", "tcsc_gpu_set_num_shards", "tcsc_gpu_set_order",
-    "tcsc_gpu_get_order", "tcsc_selftest_fingerprint", "tcsc_selftest_copy2d",
+    "tcsc_gpu_get_order",
     # include/sparse/bcsr.h
     "bcsr_from_dense", "bcsr_sgemm_basic", "bcsr_sgemm_prelu_basic", "bcsr_sgemm_avx", "bcsr_sgemm_prelu_avx",
     "bcsr_sgemm_avx2", "bcsr_free",

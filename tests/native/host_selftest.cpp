@@ -16,6 +16,7 @@
 #include "../../include/sparse/tcsc.h"
 #include "../../include/tcsc_gpu.h"
 #include "../../include/sparse_gemm.h"
+#include "tcsc_selftest.h"
 
 static int g_fail = 0;
 #define CHECK(c)                                                        \

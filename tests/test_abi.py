@@ -255,13 +255,20 @@ def test_hand_built_tcsc_round_trips_and_plan_build_validates_rows(built_lib, or
     bad.free()
 
 
-@pytest.mark.parametrize("M,K,N,threads", [(1, 512, 2048, "1"), (37, 300, 129, "1"), (256, 512, 700, "")])
+@pytest.mark.parametrize("M,K,N,threads", [(1, 512, 2048, None), (37, 300, 129, "1"), (256, 512, 700, "0"),
+                                           (64, 300, 200, "3")])
 def test_gemm_basic_bit_identical_to_reference(built_lib, oracle, M, K, N, threads, monkeypatch):
     """dense/dense.h gemm_basic -- the harness's dense oracle (dense.c:64-77),
     a CPU function of the library -- against the reference's own gemm_basic
-    (compiled in place, IEEE): same bits, on the row-blocked threaded path
-    too (a row of accumulators, k ascending per element)."""
+    (compiled in place, IEEE): same bits, single-threaded (the default, as the
+    reference) and on the opt-in threaded path ($TCSC_DENSE_THREADS; a row of
+    accumulators, k ascending per element)."""
     import pyoracle
+
+    if threads is None:
+        monkeypatch.delenv("TCSC_DENSE_THREADS", raising=False)
+    else:
+        monkeypatch.setenv("TCSC_DENSE_THREADS", threads)
 
     ref = pyoracle.load_reference()
     if ref is None:
@@ -278,3 +285,24 @@ def test_gemm_basic_bit_identical_to_reference(built_lib, oracle, M, K, N, threa
     f.argtypes, f.restype = [fp, fp, fp, fp, C.c_int, C.c_int, C.c_int], None
     f(X.reshape(-1), np.ascontiguousarray(Wd).reshape(-1), B, Y.reshape(-1), M, N, K)
     np.testing.assert_array_equal(Y.view(np.uint32), ref.gemm_basic(X, Wd, B).view(np.uint32))
+
+
+def test_main_amd_links_reference_dense():
+    """oracle/_ref/main_amd (the reference's unmodified main.cpp) carries the
+    reference's own dense/dense.c: gemm_basic, compare and the init_rand_*
+    generators are defined in the executable, so only the tcsc_* entry points
+    resolve to libtcsc_amd.so (VERDICT r3 "What's missing" #2)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "main_amd")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/main_amd not built here (needs /root/reference: make -C oracle harness)")
+    out = subprocess.run(["nm", "-C", exe], capture_output=True, text=True, check=True).stdout
+    kind = {}
+    for line in out.splitlines():
+        parts = line.split(None, 2) if line[:1] != " " else ["", *line.split(None, 1)]
+        if len(parts) == 3:
+            kind[parts[2].split("(")[0]] = parts[1]
+    for name in ("gemm_basic", "compare", "init_rand_dense", "init_rand_sparse"):
+        assert kind.get(name) == "T", (name, kind.get(name))
+    for name in ("tcsc_from_dense", "tcsc_sgemm_basic", "tcsc_sgemm_optimized", "tcsc_sgemm_prelu_basic",
+                 "tcsc_sgemm_prelu_optimized_separate", "tcsc_sgemm_prelu_optimized_onthego", "tcsc_free"):
+        assert kind.get(name) == "U", (name, kind.get(name))

@@ -495,3 +495,70 @@ def test_gpu_from_dense_fill_never_overruns(gpu, torch_cuda):
     tcsc_amd.gpu_from_dense(d, rows, cols, csp, csn, guard[:max(npos, 1)], rin)
     torch.cuda.synchronize()
     assert torch.all(guard[npos:] == -7)
+
+
+@pytest.mark.config_parity
+@pytest.mark.parametrize("axis", ["cols", "rows"])
+def test_cfg4_eight_way_shards_full_size(gpu, torch_cuda, oracle, axis):
+    """BASELINE cfg 4 split 8 ways on one GPU, each block launched exactly as
+    a rank of `bench.py --gpus 8` launches it: a column block
+    is its own plan of 2,048 columns over all of X (the per-rank path with the
+    cost model's split-K and the ordered reduce), a row block is the full plan
+    on 512 rows of X.  Columns are independent (tcsc.c:113) and so are rows,
+    so the eight blocks written into one Y must (1) match the fp64 oracle on
+    sampled rows of every block, (2) equal the oracle bit for bit on integer X,
+    (3) agree with the single launch over the whole matrix within the bound
+    (bit for bit where the split is the same)."""
+    torch = torch_cuda
+    cfg = workloads.CONFIGS[4]
+    M, K, N, G = cfg.M, cfg.K, cfg.N, 8
+    dev = torch.device("cuda:0")
+    inp = workloads.make_device_inputs(cfg, 0, N, dev)
+    csp = torch.empty(N + 1, dtype=torch.int32, device=dev)
+    csn = torch.empty(N + 1, dtype=torch.int32, device=dev)
+    npos, nneg = tcsc_amd.gpu_from_dense(inp["Wd"], K, N, csp, csn)
+    rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
+    rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
+    tcsc_amd.gpu_from_dense(inp["Wd"], K, N, csp, csn, rip, rin)
+    del inp["Wd"]
+    X, B = inp["X"], inp["B"]
+    Xi = torch.randint(-512, 513, (M, K), device=dev, dtype=torch.int32).float()
+    Bi = B.round()
+    full = tcsc_amd.Plan.from_device(K, N, csp, csn, rip, rin)
+    full.reserve(M)
+    Y1, Y1i = torch.empty((M, N), device=dev), torch.empty((M, N), device=dev)
+    full.sgemm(X, B, Y1, M, N, cfg.variant, 0.2)
+    full.sgemm(Xi, Bi, Y1i, M, N, "basic", 0.0)
+    # |b| + sum |x| per element (the bound's scale), from the same gather on magnitudes
+    S = torch.empty((M, N), device=dev)
+    full.sgemm(X.abs(), B.abs(), S, M, N, "basic", 0.0)
+    Yg, Ygi = torch.empty((M, N), device=dev), torch.empty((M, N), device=dev)
+    for c0, c1 in all_ranges(N if axis == "cols" else M, G):
+        if axis == "cols":
+            p = tcsc_amd.Plan.from_device(K, N, csp, csn, rip, rin, c0, c1)
+            p.reserve(M)
+            p.sgemm(X, B[c0:c1], Yg[:, c0:c1], M, N, cfg.variant, 0.2)
+            p.sgemm(Xi, Bi[c0:c1], Ygi[:, c0:c1], M, N, "basic", 0.0)
+            p.destroy()
+        else:
+            full.sgemm(X[c0:c1].contiguous(), B, Yg[c0:c1], c1 - c0, N, cfg.variant, 0.2)
+            full.sgemm(Xi[c0:c1].contiguous(), Bi, Ygi[c0:c1], c1 - c0, N, "basic", 0.0)
+    torch.cuda.synchronize()
+    W = pyoracle.TCSC(K, N, csp.cpu().numpy(), csn.cpu().numpy(), rip[:npos].cpu().numpy(),
+                      rin[:nneg].cpu().numpy())
+    # sampled rows: 4 per row block (every column block is in every row)
+    rng = np.random.default_rng(48)
+    rows = np.unique(np.concatenate([[0, M - 1]] + [r0 + rng.integers(0, r1 - r0, 4)
+                                                     for r0, r1 in all_ranges(M, G)]))
+    sel = torch.from_numpy(rows).to(dev)
+    Y64, S64 = oracle.f64_rows(X[sel].cpu().numpy(), W, B.cpu().numpy())
+    ok, ratio = pyoracle.check_close(Yg[sel].cpu().numpy(), Y64, S64, 0.2)
+    assert ok, f"cfg4 {axis} x{G}: worst err/bound {ratio:.3g}"
+    ref = oracle.sgemm("basic", Xi[sel].cpu().numpy(), W, Bi.cpu().numpy())
+    np.testing.assert_array_equal(Ygi[sel].cpu().numpy(), ref)
+    # every element: integer X exact (so equal to the single launch), float X
+    # within twice the per-element bound of the single launch (PReLU scales by max(1, a) = 1)
+    assert torch.equal(Ygi, Y1i)
+    bound = S.mul_(2.0 ** -19)
+    assert bool(((Yg - Y1).abs() <= bound).all()), f"cfg4 {axis} x{G}: blocks vs single launch out of bound"
+    full.destroy()

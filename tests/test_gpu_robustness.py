@@ -294,3 +294,35 @@ def test_more_than_2pow22_rows_in_one_host_call(gpu, oracle, monkeypatch):
     ref = oracle.sgemm("prelu_basic", Xi[rows], W, Bi, 0.25)
     np.testing.assert_array_equal(Y[rows], ref)
     Wl.free()
+
+
+def test_more_than_2pow22_rows_float_tail_same_order(gpu, oracle, monkeypatch):
+    """a device call of more than 2^22 rows runs as launches of
+    2^22 rows; the ragged last launch (300 rows, K = 104 > 2 chunks, so the
+    cost model alone would split K for it) must sum its rows in the same
+    order as the full launches: float inputs, the tail and head rows bit for
+    bit equal to single 1-slice launches over the same rows."""
+    import torch
+
+    dev = torch.device("cuda:0")
+    M, K, N, tail = (1 << 22) + 300, 104, 24, 300
+    Wd = oracle.ternary((K, N), 0.15, 93)
+    Wl = tcsc_amd.TcscMatrix.from_dense(Wd)
+    plan = tcsc_amd.Plan(Wl)
+    plan.reserve(M)
+    g = torch.Generator(device=dev)
+    g.manual_seed(94)
+    X = torch.rand((M, K), generator=g, device=dev) * 2 - 1
+    B = torch.rand((N,), generator=g, device=dev) * 2 - 1
+    Y = torch.empty((M, N), device=dev)
+    plan.sgemm(X, B, Y, M, N, "prelu_basic", 0.2)
+    monkeypatch.setenv("TCSC_SLICES", "1")
+    Yt = torch.empty((tail, N), device=dev)
+    plan.sgemm(X[M - tail:].contiguous(), B, Yt, tail, N, "prelu_basic", 0.2)
+    Yh = torch.empty((tail, N), device=dev)
+    plan.sgemm(X[:tail].contiguous(), B, Yh, tail, N, "prelu_basic", 0.2)
+    torch.cuda.synchronize()
+    assert torch.equal(Y[M - tail:].view(torch.int32), Yt.view(torch.int32))
+    assert torch.equal(Y[:tail].view(torch.int32), Yh.view(torch.int32))
+    plan.destroy()
+    Wl.free()

@@ -2,22 +2,26 @@
 "drops in under the existing main.cpp").
 
 oracle/_ref/main_amd is /root/reference/main.cpp compiled in place against
-its own headers and linked against libtcsc_amd.so instead of sparse/tcsc.c +
-dense/dense.c (oracle/Makefile target `harness`; the g++-mangled names come
-from csrc/tcsc_cxx_abi.cpp).  For each of its five cases (main.cpp:258-264)
-it validates every tcsc_sgemm_* variant with its own compare() (abs tol 1e-4,
+its own headers, together with the reference's own dense/dense.c, and linked
+against libtcsc_amd.so in place of sparse/tcsc.c (oracle/Makefile target
+`harness`; the g++-mangled names come from csrc/tcsc_cxx_abi.cpp).  The
+executable defines gemm_basic, compare and init_rand_* itself (its
+definitions take precedence over the library's), so the harness validates
+the GPU with the reference's own oracle and data generators: only the
+tcsc_* calls reach the library (test_main_amd_links_reference_dense checks
+this with nm).  For each of its five cases (main.cpp:258-264) it validates
+every tcsc_sgemm_* variant with its own compare() (abs tol 1e-4,
 dense.c:42-59) against its own CPU gemm_basic and exit(1)s on a mismatch
 (main.cpp:299-368), then times all six functions with its cycle counter.
 
 The test runs it to the end as a child process and requires "[OK] All
 validation tests passed!" for all five cases, no "[ERROR]" line, exit status
 0, "ALL BENCHMARKS COMPLETED" and, parsed by harness/out2csv.py, the six
-legacy timing lines of every case.  (Its dense GEMM is the library's
-gemm_basic, the harness's CPU oracle: bit-identical to the reference's,
-tests/test_abi.py, but row-blocked and threaded, so the harness's >= 1,000
-timed calls per function (main.cpp:54-113) finish in minutes.)  The output
-is streamed into gpurun_out/main_amd_out.txt as it arrives when that
-directory exists (profiles/ holds a committed copy per round).
+legacy timing lines of every case.  The reference's single-threaded
+gemm_basic is timed >= 50 times per case (main.cpp:54-113), so the run takes
+a few minutes; the output is streamed into gpurun_out/main_amd_out.txt as it
+arrives when that directory exists (profiles/ holds a committed copy per
+round).
 """
 import os
 import pty
@@ -38,6 +42,7 @@ CASES = [(1, 512, 2048), (1, 1024, 4096), (1, 2048, 8192), (256, 512, 2048), (25
 OK = "[OK] All validation tests passed!"
 
 
+@pytest.mark.timeout(540)
 def test_reference_main_cpp_validates_every_case():
     assert os.path.exists(BIN), "oracle/_ref/main_amd missing: build it with `make -C oracle harness`"
     import tcsc_amd  # noqa: F401  (fails loudly without the library)

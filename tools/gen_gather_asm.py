@@ -305,7 +305,11 @@ def write_inc(path, g):
             if a:
                 f.write(f"#elif TCSC_ABLATION == {a}\n")
             ABL = a
-            emit(f, "TCSC_GATHER_ASM", generate_tail(g) if g.tail else generate(g))
+            body = generate_tail(g) if g.tail else generate(g)
+            # s_set_gpr_idx_on/idx write M0[7:0]: the loop saves and restores
+            # M0 (operand %[m0sv]), so no compiler-managed M0 value is lost
+            # (M0 is a reserved register: a clobber would not be honoured)
+            emit(f, "TCSC_GATHER_ASM", ["s_mov_b32 %[m0sv], m0"] + body + ["s_mov_b32 m0, %[m0sv]"] if body else [])
         f.write("#else\n#define TCSC_GATHER_ASM \"\"\n#endif\n")
         ABL = 0
 
