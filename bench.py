@@ -192,7 +192,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kernel_s = ev0.elapsed_time(ev1) / 1e3 / max(args.steps, 1)
+    step_events_s = ev0.elapsed_time(ev1) / 1e3 / max(args.steps, 1)
 
     # Per-kernel split on the same stream (not part of `value`): the X^T
     # staging (k_transpose) and the gather (k_stream) back to back, each
@@ -209,9 +209,18 @@ def main():
         return a_ev.elapsed_time(b_ev) / 1e3 / n
 
     nsplit = max(args.steps, 5)
+    # the step's own kernels: k_fused (the persistent gather that writes its own
+    # X^T, + k_reduce when K is split) -- or, where the fused path does not
+    # apply, k_transpose + k_stream -- timed with HIP events on the launch stream
+    path, slices = plan.launch_info(cfg.M)
+    step_kernels_s = timed(step, nsplit)
+    # the two-kernel path of the same step, split (diagnostic, not `value`)
     transpose_s = timed(lambda: plan.prepare_x(X, cfg.M, sh), nsplit)
     plan.prepare_x(X, cfg.M, sh)
     gather_s = timed(lambda: plan.sgemm_prepared(B, Y, cfg.M, ncols, variant, 0.2, sh), nsplit)
+    kernel_s = step_kernels_s if path == "fused" else gather_s
+    kernel_name = ("k_fused" + (f" + k_reduce4 ({slices} K slices)" if slices > 1 else "")) if path == "fused" else \
+        "k_stream"
 
     alt = None
     if distributed and args.scaling == "strong" and not args.no_alt_shard and args.shard_of <= 1:
@@ -234,7 +243,7 @@ def main():
 
     if rank == 0:
         algo_bytes = workloads.algorithmic_bytes(cfg.M, cfg.K, ncols, nnz)
-        achieved = algo_bytes / gather_s / 1e9
+        achieved = algo_bytes / kernel_s / 1e9
         adds_per_launch = workloads.add_ops(cfg.M, nnz, ncols)
         traffic = None
         try:
@@ -276,13 +285,16 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "k_stream",
+                "kernel": kernel_name,
+                "path": path,
+                "k_slices": slices,
                 "algorithmic_bytes_per_launch": algo_bytes,
-                "kernel_ms": gather_s * 1e3,
-                "transpose_ms": transpose_s * 1e3,
-                "step_ms_events": kernel_s * 1e3,
-                "lds_gather_frac": (cfg.M * nnz / gather_s) / LDS_GATHER_PEAK,
-                "valu_add_frac": (adds_per_launch / gather_s) / VALU_ADD_PEAK,
+                "kernel_ms": kernel_s * 1e3,
+                "step_ms_events": step_events_s * 1e3,
+                "two_kernel_path": {"k_transpose_ms": transpose_s * 1e3, "k_stream_ms": gather_s * 1e3,
+                                    "note": "TCSC_FUSED=0 path of the same step, split (diagnostic)"},
+                "lds_gather_frac": (cfg.M * nnz / kernel_s) / LDS_GATHER_PEAK,
+                "valu_add_frac": (adds_per_launch / kernel_s) / VALU_ADD_PEAK,
             },
         }
         if validation is not None:
@@ -308,7 +320,7 @@ def main():
             }
             del Yd
         if Wd is not None and not args.no_bcsr:
-            out["bcsr"] = bcsr_line(cfg, Wd, X, B, Y, nnz, gather_s, timed, sh, nsplit)
+            out["bcsr"] = bcsr_line(cfg, Wd, X, B, Y, nnz, kernel_s, timed, sh, nsplit)
         if world == 1 and not args.no_host_api:
             # end to end through the drop-in symbol, H2D of X/B and D2H of Y
             # included (pageable numpy buffers, as main.cpp passes them); Y still holds the
@@ -330,7 +342,7 @@ def main():
             for v in ("prelu_basic", "prelu_separate"):
                 rplan.sgemm_prepared(B, Y, cfg.M, ncols, v, 0.2, sh)
                 t = timed(lambda: rplan.sgemm_prepared(B, Y, cfg.M, ncols, v, 0.2, sh), nsplit)
-                ref[v] = {"ms": t * 1e3, "g_add_ops_per_s": adds_per_launch / t / 1e9, "vs_fast_order": t / gather_s}
+                ref[v] = {"ms": t * 1e3, "g_add_ops_per_s": adds_per_launch / t / 1e9, "vs_fast_order": t / kernel_s}
             rplan.destroy()
             out["reference_order"] = ref
         if world == 1 and not args.no_graph:
@@ -462,8 +474,6 @@ def other_configs(args, tcsc_amd, workloads, dev, sh, timed, skip):
         del inp["Wd"]
         plan = tcsc_amd.Plan.from_device(c.K, c.N, csp, csn, rip, rin, 0, c.N, dev.index or 0, sh)
         plan.reserve(c.M)
-        info = plan.info()
-        mfma_min = info["mfma_min_M"]
         Yc = torch.empty((c.M, c.N), device=dev)
 
         def one():
@@ -473,9 +483,12 @@ def other_configs(args, tcsc_amd, workloads, dev, sh, timed, skip):
             one()
         t = timed(one, 30)
         nnz = npos + nneg
-        mfma = bool(mfma_min and c.M >= mfma_min)
-        path = ("mfma (bf16 x3 split GEMM)" if mfma else
-                "small-M (one wave per column)" if c.M <= 16 else "gather (k_stream)")
+        lpath, lslices = plan.launch_info(c.M)
+        mfma = lpath == "mfma"
+        path = {"mfma": "mfma (bf16 x3 split GEMM: k_split3 + k_gemm3)", "small": "small-M (one wave per column)",
+                "fused": "fused gather (k_fused: X^T written in the same launch)",
+                "gather": "gather (k_transpose + k_stream)"}[lpath] + \
+            (f", K split {lslices} ways + k_reduce4" if lslices > 1 else "")
         r = {
             "workload": c.describe(), "variant": c.variant, "nnz": nnz, "ms": t * 1e3,
             "g_add_ops_per_s": workloads.add_ops(c.M, nnz, c.N) / t / 1e9,

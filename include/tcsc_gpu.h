@@ -110,6 +110,22 @@ int tcsc_gpu_plan_create_device(int rows, int cols,
 
 int tcsc_gpu_plan_get_info(const tcsc_gpu_plan *plan, tcsc_gpu_plan_info *info);
 
+/* Which kernels a tcsc_gpu_sgemm of M rows on this plan runs (with X 16-B
+ * aligned, the plan's reserved workspace and the current environment):
+ *   TCSC_PATH_FUSED  k_fused: X^T written by the gather's own workgroups
+ *                    (one persistent launch, + k_reduce when K is split)
+ *   TCSC_PATH_GATHER k_transpose + k_stream (+ k_reduce)
+ *   TCSC_PATH_MFMA   k_split3 + k_gemm3 (+ k_fixup), near-dense W
+ *   TCSC_PATH_SMALL  k_small_m, M <= 16
+ * and *slices = the K split of the gather paths (1 = none). */
+enum tcsc_path {
+    TCSC_PATH_GATHER = 0,
+    TCSC_PATH_FUSED = 1,
+    TCSC_PATH_MFMA = 2,
+    TCSC_PATH_SMALL = 3
+};
+int tcsc_gpu_launch_info(const tcsc_gpu_plan *plan, int M, int *path, int *slices);
+
 /* Allocate the plan's workspace for launches of up to `max_M` rows: X^T
  * (K x max_M rounded up to 256 floats; the kernel streams X^T rows into LDS)
  * plus, where the cost model splits K over workgroups, the fp32 partial

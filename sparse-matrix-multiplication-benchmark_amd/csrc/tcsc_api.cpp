@@ -71,6 +71,12 @@ struct tcsc_gpu_plan {
     int *ccp = nullptr, *ccn = nullptr, *crp = nullptr, *crn = nullptr;
     size_t csc_bytes = 0;
     int mfma_min_M = 0;
+    // the fused persistent gather's synchronisation block (tcsc::fused_sync_bytes
+    // for up to fsync_M rows; zeroed once, never reset: the counters carry
+    // the launch epoch) and the persistent grid size
+    unsigned* fsync = nullptr;
+    int fsync_M = 0;
+    int num_cus = 0;
 };
 
 namespace {
@@ -622,6 +628,12 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
     g.ws_bytes = g.ws ? ws_bytes - xtb : 0;
     g.force_slices = force_slices > 0 ? force_slices : slices_override();
     g.stage = stage;
+    // the plan's own workspace (device API) with its synchronisation block:
+    // the fused persistent kernel (tcsc::launch_gemm decides if it applies)
+    if (ws == p->ws && p->fsync && M <= p->fsync_M) {
+        g.fsync = p->fsync;
+        g.num_cus = p->num_cus;
+    }
     // Bias first for tcsc_sgemm_basic (tcsc.c:74-96), last otherwise
     // (tcsc.c:149-161; the optimized family adds per-sign partial sums to
     // the bias, which no single accumulation order reproduces: DESIGN.md).
@@ -784,6 +796,7 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan* p) {
     if (p->ent) (void)hipFree(p->ent);
     if (p->sptr) (void)hipFree(p->sptr);
     if (p->ws) (void)hipFree(p->ws);
+    if (p->fsync) (void)hipFree(p->fsync);
     free_mfma(p);
     free_csc(p);
     tcsc_gpu_plan_destroy(p->chain_pos);
@@ -803,6 +816,21 @@ int tcsc_gpu_plan_reserve(tcsc_gpu_plan* p, int max_M) {
                                           slices_override());
         want = std::max(want, tcsc::xt_bytes(max_M, p->rows) + tcsc::workspace_bytes(max_M, p->cols, s));
     }
+    if (max_M > p->fsync_M && p->rows > 0 && p->order == TCSC_ORDER_FAST) {
+        DeviceGuard dg(p->device);
+        if (p->fsync) {
+            HIP_TRY(hipDeviceSynchronize());  // a queued launch may still use it
+            (void)hipFree(p->fsync);
+            p->fsync = nullptr;
+            p->fsync_M = 0;
+        }
+        const size_t fb = tcsc::fused_sync_bytes(max_M, p->rows);
+        HIP_TRY(hipMalloc(&p->fsync, fb));
+        HIP_TRY(hipMemset(p->fsync, 0, fb));
+        HIP_TRY(hipDeviceSynchronize());
+        p->fsync_M = max_M;
+        if (!p->num_cus) HIP_TRY(hipDeviceGetAttribute(&p->num_cus, hipDeviceAttributeMultiprocessorCount, p->device));
+    }
     if (want <= p->ws_bytes) return TCSC_OK;
     DeviceGuard dg(p->device);
     if (p->ws) {
@@ -817,6 +845,41 @@ int tcsc_gpu_plan_reserve(tcsc_gpu_plan* p, int max_M) {
     return TCSC_OK;
 }
 
+
+int tcsc_gpu_launch_info(const tcsc_gpu_plan* p, int M, int* path, int* slices) {
+    if (!p || M < 0 || !path || !slices) {
+        set_error("tcsc_gpu_launch_info: bad arguments");
+        return TCSC_E_ARG;
+    }
+    *slices = 1;
+    if (use_mfma(p, M)) {
+        *path = TCSC_PATH_MFMA;
+        return TCSC_OK;
+    }
+    if (use_small(p, M)) {
+        *path = TCSC_PATH_SMALL;
+        return TCSC_OK;
+    }
+    const int rows = std::min(M, 1 << 22);  // one launch of at most 2^22 rows (sgemm_ws)
+    const size_t xtb = tcsc::xt_bytes(rows, p->rows);
+    tcsc::GemmArgs g;
+    g.X = reinterpret_cast<const float*>(p->ws);  // any 16-B aligned X
+    g.M = rows;
+    g.K = p->rows;
+    g.ncols = p->cols;
+    g.stage = 0;
+    g.order = p->order == TCSC_ORDER_REFERENCE ? 1 : 0;
+    if (p->fsync && rows <= p->fsync_M) {
+        g.fsync = p->fsync;
+        g.num_cus = p->num_cus;
+    }
+    *path = tcsc::fused_eligible(g) ? TCSC_PATH_FUSED : TCSC_PATH_GATHER;
+    if (g.order == 0)
+        *slices = M > (1 << 22) ? 1
+                                : tcsc::choose_slices(rows, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups,
+                                                      p->ws_bytes > xtb ? p->ws_bytes - xtb : 0, slices_override());
+    return TCSC_OK;
+}
 
 int tcsc_gpu_sgemm(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy,
                    int variant, float a, void* stream) {

@@ -162,6 +162,58 @@ struct PlanOut {
     size_t scan_tmp_bytes = 0;
 };
 
+// ---- the fused persistent gather (k_fused, DESIGN.md §4 "k_fused") --------
+// X^T is written by the same launch that gathers from it: the output tiles
+// (row tile rt, K slice z, column block cb) are items of a persistent grid,
+// grouped by (rt, z); the group's workgroups transpose its rows of X in
+// units of 4 k rows x 256 m (one LDS-DMA of 4 x 1 KiB, four 1-KiB stores)
+// a few pieces ahead of their own gather, and signal per piece of
+// kFusedPieceChunks chunks on a counter {epoch, count}.
+constexpr int kUnitK = 4;                        // k rows per transposition unit
+constexpr int kUnitsPerChunk = kTK / kUnitK;     // 12
+constexpr int kUnitBytes = kTM * kUnitK * 4;     // 4 KiB of LDS staging per unit
+static_assert(kTK % kUnitK == 0, "whole units per chunk");
+constexpr int kProdWave0 = 4;                    // producer waves 4, 5 (one LDS slot each)
+constexpr int kProdWaves = 2;
+constexpr int kPollWave = 6;                     // polls the piece counters
+// LDS: the ring, one 256-B landing area that every wave's stream prefetch
+// shares (the data is never read), the producer slots, the item record
+constexpr int kFusedPfOff = kRingBytes;
+constexpr int kFusedSlotOff = kFusedPfOff + 256;
+constexpr int kFusedStateOff = kFusedSlotOff + kProdWaves * kUnitBytes;
+constexpr int kFusedStateBytes = 128;  // item record (64 B) + producer states (16 B each)
+constexpr int kFusedLdsBytes0 = kFusedStateOff + kFusedStateBytes;
+constexpr int kFusedLdsBytes = kFusedLdsBytes0 > kEpiMinBytes ? kFusedLdsBytes0 : kEpiMinBytes;
+static_assert(kFusedLdsBytes <= 160 * 1024, "fused kernel LDS");
+// synchronisation block of a plan (device memory, zeroed once): [0] the
+// epoch of the last completed launch, [1] arrivals of the running launch,
+// then 64-bit piece counters, one per (row tile, chunk) of the largest
+// launch the block was sized for
+constexpr size_t kFusedSyncHdr = 256;
+inline size_t fused_sync_bytes(int M, int K) {
+    const size_t nrt = (size_t)(M + kTM - 1) / kTM, nch = (size_t)(K + kTK - 1) / kTK;
+    return kFusedSyncHdr + nrt * (nch > 0 ? nch : 1) * 8;
+}
+
+struct FusedArgs {
+    const float* X = nullptr;       // M x K row-major
+    float* XT = nullptr;            // (K + look-ahead) x ldxt workspace
+    int M = 0, K = 0, ldxt = 0;
+    const int2* ent = nullptr;
+    const int* sptr = nullptr;
+    long long n_entries = 0;
+    int G = 0, ncols = 0, nch = 0, cps = 0, Z = 1, ncb = 0, n_items = 0;
+    const float* Bias = nullptr;
+    float* Y = nullptr;
+    int ldy = 0;
+    float a = 0.f;
+    float* ws = nullptr;            // split-K slabs (Z > 1)
+    int pf_dist = 0, pf_lines = 1;
+    unsigned* sync = nullptr;       // fused_sync_bytes(M, K) block
+    int pc = 8;                     // chunks per piece
+    int lead = 2;                   // pieces produced before an item's gather starts
+};
+
 struct GemmArgs {
     const float* X = nullptr;
     float* XT = nullptr;       // K x ldxt workspace: X transposed (ldxt = M rounded up to kTM)
@@ -186,8 +238,12 @@ struct GemmArgs {
     bool prelu = false;
     float* ws = nullptr;       // split-K partial slabs (may be null: no split)
     size_t ws_bytes = 0;
-    int force_slices = 0;
-    int stage = 0;             // 0: transpose + gather, 1: transpose only, 2: gather only (X^T prepared)      // 0 = cost model
+    int force_slices = 0;      // 0 = cost model
+    int stage = 0;             // 0: transpose + gather, 1: transpose only, 2: gather only (X^T prepared)
+    // stage 0 only: the plan's synchronisation block (fused_sync_bytes for at
+    // least this M) enables the fused persistent kernel; null = k_transpose + k_stream
+    unsigned* fsync = nullptr;
+    int num_cus = 0;           // persistent grid size (workgroups, one per CU)
 };
 
 // Plan building
@@ -202,6 +258,8 @@ void pf_stream_params(long long n_entries, int n_groups, int n_chunks, int* dist
 size_t workspace_bytes(int M, int ncols, int slices);
 size_t xt_bytes(int M, int K);
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st);
+// whether launch_gemm takes the fused persistent kernel for these arguments
+bool fused_eligible(const GemmArgs& g);
 // tcsc_from_dense on the device
 // tile counts cp/cn ([row tile][col], dense_tile_rows(rows) rows per tile)
 // turned into per-column tile offsets in place; column totals into totp/totn

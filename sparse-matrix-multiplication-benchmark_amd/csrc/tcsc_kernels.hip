@@ -767,6 +767,552 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     }
 }
 
+// ---------------------------------------------------------------------------
+// K1f: k_fused -- the persistent gather with the X^T staging fused in
+// ---------------------------------------------------------------------------
+// One workgroup per CU (the grid is the chip's resident capacity) loops over
+// items (row tile rt, K slice z, column block cb) numbered group-major, item
+// = (rt*Z + z)*ncb + cb: the ncb items of one group (rt, z) -- the column
+// blocks that stream the same rows of X^T -- are consecutive and, through
+// the XCD-aware slot order, run at once on one XCD (the L2 sharing of
+// k_stream's tile order).  Instead of a k_transpose launch ahead of the
+// gather, the group's workgroups write its rows of X^T themselves while they
+// gather (the transpose is HBM-bound, the gather LDS-bound):
+//  * a unit is 4 k rows x 256 m: an LDS-DMA of 4 x 1 KiB (lane l: X rows
+//    m0+4l..4l+3, k0..k0+3) into a 4-KiB slot, ds_read_b128 x 4, a 4 x 4
+//    transpose in registers, 4 x global_store_dwordx4 sc1 (1-KiB rows of X^T);
+//  * the group's members (its items in the group's first round of the grid)
+//    have two producer agents each (waves 4 and 5); agent a of An produces
+//    the units u = a, a + An, ... of the group's K range; a piece is pc
+//    chunks (12*pc units); an agent adds 1 to a piece's counter once its
+//    units of the piece are stored and complete (s_waitcnt vmcnt, then an
+//    agent-scope atomic);
+//  * an item first produces its units of the first `lead` pieces (all of
+//    them when the group has too few members to stay ahead), then every
+//    producer wave produces one unit per chunk (the LDS-DMA issued after
+//    gather(c) is consumed after gather(c+1), one slot per wave after the
+//    ring);
+//  * before the barrier that precedes the DMA of a piece's first chunk, wave
+//    6 polls the piece's counter until it reads {this launch's epoch, the
+//    piece's agent count}; the barrier then orders every wave's loads of
+//    those rows after the poll (MI355X_MICROARCH.md, inter-workgroup
+//    visibility: sc1 stores drained by vmcnt, agent atomic, sc1 poll,
+//    workgroup barrier).
+// The counters carry the launch's epoch in their upper half and are never
+// reset: every workgroup reads the epoch of the last completed launch from
+// the plan's sync block at entry, and the last workgroup to finish (an
+// atomicInc that wraps back to 0) advances it, so a captured graph replays
+// correctly.  A wait longer than kPollLimit polls (a member that is not
+// resident: the GPU shared with another kernel) makes the waiting workgroup
+// produce the piece itself (the same values; writes are idempotent).
+constexpr int kPollLimit = 1 << 12;
+
+__device__ __forceinline__ int xcd_slot(int b, int P) {
+    const int q = P >> 3, r = P & 7, x = b & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+__device__ __forceinline__ void piece_signal(unsigned long long* c, unsigned e) {
+    unsigned long long v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        const unsigned long long nv = (unsigned)(v >> 32) == e ? v + 1ull : (((unsigned long long)e << 32) | 1ull);
+        if (__hip_atomic_compare_exchange_strong(c, &v, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            return;
+    }
+}
+
+__device__ __forceinline__ bool piece_ready(unsigned long long* c, unsigned e, unsigned tgt) {
+    const unsigned long long v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    return hi == e && lo >= tgt;
+}
+
+// LDS-DMA of unit (X rows m0 .. m0+255, k0 .. k0+3) into LDS at `slot`:
+// instruction r writes slot + r KiB, lane l X[min(m0+4l+r, M-1)][k0 .. k0+3].
+__device__ __forceinline__ void unit_dma(const float* X, int K, int M, int m0, int k0, unsigned slot, int lane) {
+    const char* base = reinterpret_cast<const char*>(X + (size_t)m0 * K + k0);
+    const int mmax = M - 1 - m0;
+    unsigned off[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) off[r] = (unsigned)min(4 * lane + r, mmax) * (unsigned)K * 4u;
+    unsigned sv;
+    asm volatile("s_mov_b32 %[sv], m0\n\t"
+                 "s_mov_b32 m0, %[s0]\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o0], %[b]\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o1], %[b]\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o2], %[b]\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o3], %[b]\n\t"
+                 "s_mov_b32 m0, %[sv]"
+                 : [sv] "=&s"(sv)
+                 : [s0] "s"(slot), [o0] "v"(off[0]), [o1] "v"(off[1]), [o2] "v"(off[2]), [o3] "v"(off[3]),
+                   [b] "s"(base)
+                 : "memory", "scc");
+}
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// X^T rows k0 .. k0+3, columns m0 .. m0+255 from the unit staged at lds + slot
+// (ds_read_b128 x 4, the 4 x 4 block of lane l transposed in registers,
+// 4 x global_store_dwordx4 sc1: write-through, so no L2 write-back is needed
+// before the piece is signalled).
+__device__ __forceinline__ void unit_store(const char* lds_slot, float* XT, int ldxt, int m0, int k0, int lane) {
+    const f32x4v* s = reinterpret_cast<const f32x4v*>(lds_slot) + lane;
+    const f32x4v x0 = s[0], x1 = s[64], x2 = s[128], x3 = s[192];
+    char* base = reinterpret_cast<char*>(XT + (size_t)k0 * ldxt + m0);
+    const unsigned o = 16u * lane, st = (unsigned)ldxt * 4u;
+    const f32x4v r0 = {x0.x, x1.x, x2.x, x3.x}, r1 = {x0.y, x1.y, x2.y, x3.y};
+    const f32x4v r2 = {x0.z, x1.z, x2.z, x3.z}, r3 = {x0.w, x1.w, x2.w, x3.w};
+    asm volatile("global_store_dwordx4 %0, %1, %2 sc1" ::"v"(o), "v"(r0), "s"(base) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, %2 sc1" ::"v"(o + st), "v"(r1), "s"(base) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, %2 sc1" ::"v"(o + 2 * st), "v"(r2), "s"(base) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, %2 sc1" ::"v"(o + 3 * st), "v"(r3), "s"(base) : "memory");
+}
+
+// The same unit through registers (the timeout path: one wave, no LDS).
+__device__ __forceinline__ void unit_direct(const float* X, int K, int M, float* XT, int ldxt, int m0, int k0,
+                                            int lane) {
+    const int mmax = M - 1 - m0;
+    f32x4v x[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        x[r] = *reinterpret_cast<const f32x4v*>(X + (size_t)(m0 + min(4 * lane + r, mmax)) * K + k0);
+    char* base = reinterpret_cast<char*>(XT + (size_t)k0 * ldxt + m0);
+    const unsigned o = 16u * lane, st = (unsigned)ldxt * 4u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const f32x4v v = {x[0][j], x[1][j], x[2][j], x[3][j]};
+        asm volatile("global_store_dwordx4 %0, %1, %2 sc1" ::"v"(o + j * st), "v"(v), "s"(base) : "memory");
+    }
+}
+
+// The kernel's arguments, re-read from the kernarg segment at each use
+// (s_load, scalar-cache hits): an opaque copy of the segment pointer keeps
+// the compiler from holding every field in SGPRs across the chunk loop, where
+// the gather pins 54 of them.
+typedef __attribute__((address_space(4))) const FusedArgs cFusedArgs;
+__device__ __forceinline__ cFusedArgs* fargs() {
+    cFusedArgs* p = (cFusedArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+// Item record in LDS (written by wave 0 at each item's start, read by the
+// producer and poll waves inside the chunk loop, so none of it is live in
+// registers across the gather): dwords
+//   0-1 X + m0*K (bytes)   2-3 XT + m0 (bytes)   4 K   5 M-1-m0   6 ldxt   7 k_lo
+//   8 U (units)   9 units per piece   10 An (agents)   11 epoch   12 log2(pc)   13 chunks
+//   14-15 the counter of piece 0
+// Producer state (waves 4, 5), dwords: 0 next unit (INT_MAX: none left),
+// 1 unit in the slot (-1: none), 2 unit whose stores were issued last (-1).
+struct ItemRec {
+    unsigned long long xrow, xtrow;
+    int K, mmax, ldxt, k_lo, U, upc, An;
+    unsigned e;
+    int pcs, nloc;  // log2(chunks per piece), chunks of the item
+    unsigned long long crow;
+};
+static_assert(sizeof(ItemRec) == 64, "item record layout");
+
+__device__ __forceinline__ ItemRec load_rec(const char* lds) {
+    const int4* q = reinterpret_cast<const int4*>(lds + kFusedStateOff);
+    const int4 a = q[0], b = q[1], c = q[2], d = q[3];
+    ItemRec r;
+    r.xrow = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(a.y) << 32) |
+             (unsigned)__builtin_amdgcn_readfirstlane(a.x);
+    r.xtrow = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(a.w) << 32) |
+              (unsigned)__builtin_amdgcn_readfirstlane(a.z);
+    r.K = __builtin_amdgcn_readfirstlane(b.x);
+    r.mmax = __builtin_amdgcn_readfirstlane(b.y);
+    r.ldxt = __builtin_amdgcn_readfirstlane(b.z);
+    r.k_lo = __builtin_amdgcn_readfirstlane(b.w);
+    r.U = __builtin_amdgcn_readfirstlane(c.x);
+    r.upc = __builtin_amdgcn_readfirstlane(c.y);
+    r.An = __builtin_amdgcn_readfirstlane(c.z);
+    r.e = (unsigned)__builtin_amdgcn_readfirstlane(c.w);
+    r.pcs = __builtin_amdgcn_readfirstlane(d.x);
+    r.nloc = __builtin_amdgcn_readfirstlane(d.y);
+    r.crow = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(d.w) << 32) |
+             (unsigned)__builtin_amdgcn_readfirstlane(d.z);
+    return r;
+}
+
+// One production step of a producer wave: the unit issued last time lands
+// (its LDS-DMA had a chunk of gather to arrive), is transposed and stored;
+// the stores issued last time are complete, so their piece is signalled if
+// they were this agent's last units of it; the next unit's DMA is issued.
+// `drain` waits for everything (the flush after the chunk loop).
+__device__ __forceinline__ void produce_step(char* lds, int wave, int lane, bool drain) {
+    int4* stp = reinterpret_cast<int4*>(lds + kFusedStateOff + 64) + (wave - kProdWave0);
+    const int4 st = *stp;
+    int u_next = __builtin_amdgcn_readfirstlane(st.x), slot_u = __builtin_amdgcn_readfirstlane(st.y),
+        sig_u = __builtin_amdgcn_readfirstlane(st.z);
+    if (u_next == 0x7fffffff && slot_u < 0 && sig_u < 0) return;
+    const ItemRec r = load_rec(lds);
+    if (drain)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else  // all but this chunk's stream prefetch
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    unsigned long long* crow = reinterpret_cast<unsigned long long*>(r.crow);
+    if (sig_u >= 0) {
+        const int p = sig_u / r.upc;
+        if (sig_u + r.An >= min(r.U, (p + 1) * r.upc) && lane == 0) piece_signal(crow + ((size_t)p << r.pcs), r.e);
+        sig_u = -1;
+    }
+    const float* X = reinterpret_cast<const float*>(r.xrow);
+    float* XT = reinterpret_cast<float*>(r.xtrow);
+    const char* slot_ptr = lds + kFusedSlotOff + (wave - kProdWave0) * kUnitBytes;
+    if (slot_u >= 0) {
+        unit_store(slot_ptr, XT + (size_t)(r.k_lo + kUnitK * slot_u) * r.ldxt, r.ldxt, 0, 0, lane);
+        sig_u = slot_u;
+        slot_u = -1;
+    }
+    if (u_next < r.U) {
+        unit_dma(X + r.k_lo + kUnitK * u_next, r.K, r.mmax + 1, 0, 0,
+                 (unsigned)reinterpret_cast<uintptr_t>(slot_ptr), lane);
+        slot_u = u_next;
+        u_next = u_next + r.An < r.U ? u_next + r.An : 0x7fffffff;
+    } else {
+        u_next = 0x7fffffff;
+    }
+    if (lane == 0) *stp = make_int4(u_next, slot_u, sig_u, 0);
+}
+
+// Wave 6 before the barrier ahead of chunk c+kNBuf-1's DMA: when that chunk
+// opens a piece, wait until the piece's counter is complete.  Past
+// kPollLimit polls (a member that is not running) the wave writes the
+// piece's X^T rows itself.
+__device__ __forceinline__ void wait_piece(const char* lds, int p, int lane) {
+    const ItemRec r = load_rec(lds);
+    unsigned long long* c = reinterpret_cast<unsigned long long*>(r.crow) + ((size_t)p << r.pcs);
+    const unsigned tgt = (unsigned)min(r.An, min(r.U, (p + 1) * r.upc) - p * r.upc);
+    for (int n = 0; !piece_ready(c, r.e, tgt); ++n) {
+        if (n > kPollLimit) {
+            const float* X = reinterpret_cast<const float*>(r.xrow);
+            float* XT = reinterpret_cast<float*>(r.xtrow);
+            const int u1 = min(r.U, (p + 1) * r.upc);
+            for (int u = p * r.upc; u < u1; ++u)
+                unit_direct(X + r.k_lo + kUnitK * u, r.K, r.mmax + 1, XT + (size_t)(r.k_lo + kUnitK * u) * r.ldxt,
+                            r.ldxt, 0, 0, lane);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// Opaque copies: the value is the same, but the compiler cannot hoist what
+// is derived from it out of the loop it is made in.  k_fused makes its lane
+// and wave numbers opaque at the start of every phase of an item, so values
+// a phase derives from them are computed in that phase instead of before the
+// item loop (where they would stay live across every gather: spills).
+__device__ __forceinline__ int opaque_v(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ int opaque_s(int x) {
+    asm volatile("" : "+s"(x));
+    return x;
+}
+
+struct ItemPos {
+    int rt, z, cb, grp, m0, c_begin, c_end;
+};
+__device__ __forceinline__ ItemPos item_pos(int item) {
+    cFusedArgs* F = fargs();
+    ItemPos q;
+    q.grp = item / F->ncb;
+    q.cb = item - q.grp * F->ncb;
+    q.rt = q.grp / F->Z;
+    q.z = q.grp - q.rt * F->Z;
+    q.m0 = q.rt * kTM;
+    q.c_begin = q.z * F->cps;
+    q.c_end = min(F->nch, q.c_begin + F->cps);
+    return q;
+}
+
+template <bool BIAS_FIRST, bool PRELU, int OUT>
+__global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const FusedArgs A) {
+    __shared__ __attribute__((aligned(16))) char lds[kFusedLdsBytes];
+    (void)A;  // every field is read through fargs()
+    {
+        // the epoch of this launch: the last completed launch's + 1
+        unsigned* sync = fargs()->sync;
+        const unsigned e = (unsigned)__builtin_amdgcn_readfirstlane(
+            (int)(__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u));
+        if (threadIdx.x == 0) reinterpret_cast<unsigned*>(lds + kFusedStateOff)[11] = e;
+    }
+
+    for (int item = xcd_slot(blockIdx.x, gridDim.x); item < fargs()->n_items; item = opaque_s(item + (int)gridDim.x)) {
+        // ---- item prologue: this agent's units of the first `lead` pieces, the record, piece 0 ----
+        {
+            const int lane = opaque_v(threadIdx.x & 63);
+            const int wave = opaque_s(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+            const bool prod_wave = wave >= kProdWave0 && wave < kProdWave0 + kProdWaves;
+            const int P = gridDim.x;
+            const ItemPos q = item_pos(item);
+            cFusedArgs* F = fargs();
+            const int ncb = F->ncb, nch = F->nch, K = F->K, M = F->M;
+            // the group's members: its items in the group's first round
+            const int gi0 = q.grp * ncb;
+            const int mem_end = min(gi0 + ncb, (gi0 / P + 1) * P);
+            const int An = kProdWaves * (mem_end - gi0);
+            const int k_lo = q.c_begin * kTK;
+            const int U = q.c_begin < q.c_end ? (min(q.c_end * kTK, K) - k_lo + kUnitK - 1) / kUnitK : 0;
+            const int pc = F->pc, upc = kUnitsPerChunk * pc;
+            const int npieces = (U + upc - 1) / upc;
+            // every piece up front when the members cannot keep ahead (one unit
+            // per chunk and agent against the group's 12 units per chunk)
+            const int lead = (An * 10 < kUnitsPerChunk * 11) ? npieces : min(F->lead, npieces);
+            const int agent = (item < mem_end && prod_wave) ? kProdWaves * (item - gi0) + (wave - kProdWave0) : -1;
+            unsigned long long* const crow =
+                reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(F->sync) + kFusedSyncHdr) +
+                (size_t)q.rt * nch + q.c_begin;
+            const float* Xr = F->X + (size_t)q.m0 * K;
+            float* XTr = F->XT + q.m0;
+            const int ldxt = F->ldxt;
+            __syncthreads();  // the previous item's epilogue is done with the LDS
+            int4* rec4 = reinterpret_cast<int4*>(lds + kFusedStateOff);
+            const unsigned e = (unsigned)__builtin_amdgcn_readfirstlane(rec4[2].w);
+            int u_next = agent;
+            if (agent >= 0) {
+                const int lead_units = min(U, lead * upc);
+                constexpr int half = kRingBytes / 2 / kUnitBytes;  // ring slots per producer wave
+                const int slot0 = (wave - kProdWave0) * half * kUnitBytes;
+                while (u_next < lead_units) {
+                    int nb = 0;
+                    for (int u = u_next; u < lead_units && nb < half; u += An, ++nb)
+                        unit_dma(Xr + k_lo + kUnitK * u, K, M - q.m0, 0, 0,
+                                 (unsigned)reinterpret_cast<uintptr_t>(lds) + slot0 + nb * kUnitBytes, lane);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    for (int i = 0; i < nb; ++i, u_next += An)
+                        unit_store(lds + slot0 + i * kUnitBytes, XTr + (size_t)(k_lo + kUnitK * u_next) * ldxt, ldxt, 0,
+                                   0, lane);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0)
+                    for (int p = 0; p < lead; ++p) {
+                        const int f = p * upc + (((agent - p * upc) % An) + An) % An;  // the agent's first unit in p
+                        if (f < min(U, (p + 1) * upc)) piece_signal(crow + (size_t)p * pc, e);
+                    }
+            }
+            if (prod_wave && lane == 0)
+                reinterpret_cast<int4*>(lds + kFusedStateOff + 64)[wave - kProdWave0] =
+                    make_int4(agent >= 0 && u_next < U ? u_next : 0x7fffffff, -1, -1, 0);
+            if (wave == 0 && lane == 0) {
+                const unsigned long long xr = reinterpret_cast<unsigned long long>(Xr);
+                const unsigned long long xtr = reinterpret_cast<unsigned long long>(XTr);
+                const unsigned long long cr = reinterpret_cast<unsigned long long>(crow);
+                rec4[0] = make_int4((int)xr, (int)(xr >> 32), (int)xtr, (int)(xtr >> 32));
+                rec4[1] = make_int4(K, M - 1 - q.m0, ldxt, k_lo);
+                rec4[2] = make_int4(U, upc, An, (int)e);
+                rec4[3] = make_int4(31 - __builtin_clz(pc), q.c_end - q.c_begin, (int)cr, (int)(cr >> 32));
+            }
+            __syncthreads();  // the record, before the first wait
+            if (wave == kPollWave && npieces > 0) wait_piece(lds, 0, lane);
+            __syncthreads();
+        }
+
+        facc_t acc[TCSC_ACC_VECS];
+#pragma unroll
+        for (int v = 0; v < TCSC_ACC_VECS; ++v)
+#pragma unroll
+            for (int i = 0; i < TCSC_ACC_W; ++i) acc[v][i] = 0.f;
+
+        // ---- the chunk loop (k_stream's) ----
+        {
+            const int lane = opaque_v(threadIdx.x & 63);
+            const int wave = opaque_s(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+            const ItemPos q = item_pos(item);
+            const int g = q.cb * kWaves + wave;
+            cFusedArgs* F = fargs();
+            const bool active = g < F->G;
+            if (BIAS_FIRST && OUT == 0 && active) {
+                const int cbias = group_col0(g) + lane;
+                const float bv = (lane < wave_cols(wave) && cbias < F->ncols) ? F->Bias[cbias] : 0.f;
+#pragma unroll
+                for (int j = 0; j < kCW; ++j) {
+                    const float b = __shfl(bv, j);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc_set(acc, 4 * j + r, b);
+                }
+            }
+            // the -0.0 pad row of every ring buffer (the prologue's production used the ring)
+            if (threadIdx.x < 64 * kNBuf) {
+                const int b = threadIdx.x >> 6;
+                reinterpret_cast<float4*>(lds + (b * kBufRows + kTK) * kRowBytes)[lane] =
+                    make_float4(-0.f, -0.f, -0.f, -0.f);
+            }
+            const int c_begin = q.c_begin, c_end = q.c_end;
+            if (c_begin < c_end) {
+                const bool prod_wave = wave >= kProdWave0 && wave < kProdWave0 + kProdWaves;
+                DmaState dma;
+                const int ldxt = F->ldxt;
+                dma.chunk_bytes = (size_t)kTK * ldxt * 4;
+                dma.next = reinterpret_cast<const char*>(F->XT + (size_t)c_begin * kTK * ldxt + q.m0);
+#pragma unroll
+                for (int i = 0; i < kDmaPerWave; ++i)
+                    dma.voff[i] = 16u * lane + (unsigned)((wave * kDmaPerWave + i) * ldxt * 4) -
+                                  (TCSC_DMA_OFFSET ? (unsigned)((i % 4) * kRowBytes) : 0u);
+                dma.lds_wave = (unsigned)reinterpret_cast<uintptr_t>(lds) + (unsigned)(wave * kDmaPerWave * kRowBytes);
+                const bool dma_wave = wave < kDmaWaves;
+                const int buf0 = c_begin % kNBuf;
+                const unsigned pf_m0 = (unsigned)reinterpret_cast<uintptr_t>(lds) + kFusedPfOff;
+                const unsigned pf_s_off = (unsigned)F->pf_dist + 128u * (unsigned)(lane * F->pf_lines >> 6);
+                // (a vector load: the kernel stores to global memory, so the
+                // compiler cannot prove sptr unchanged for a scalar load)
+                const long long s0 =
+                    active ? (long long)__builtin_amdgcn_readfirstlane(F->sptr[(long long)g * F->nch + c_begin])
+                           : F->n_entries;
+                unsigned long long cur = reinterpret_cast<unsigned long long>(F->ent + s0);
+                auto pf_issue = [&](unsigned long long p) {
+                    if (kPfS) pf_touch(pf_m0, pf_s_off, reinterpret_cast<const char*>(p));
+                };
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // pad rows
+                if (dma_wave) dma_next_chunk(dma, buf0);
+                i32x16 sb[TCSC_SBUF_VECS];
+                sbuf_tail_t sbt;
+                load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
+                pf_issue(cur);
+#pragma unroll
+                for (int i = 1; i + 1 < kNBuf; ++i) {
+                    if (dma_wave) dma_next_chunk(dma, (buf0 + i) % kNBuf);
+                    pf_issue(cur);
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const unsigned mask = 0x3ffu;
+                int dbuf = (buf0 + kNBuf - 1) % kNBuf;
+                for (int c = c_begin; c < c_end; ++c) {
+                    if (wave == kPollWave) {  // chunk c+kNBuf-1 is DMA'd right after this barrier
+                        const int* rec = reinterpret_cast<const int*>(lds + kFusedStateOff);
+                        const int pcs = __builtin_amdgcn_readfirstlane(rec[12]);  // log2(pc)
+                        const int t2 = c + kNBuf - 1 - c_begin;
+                        if (t2 < c_end - c_begin && (t2 & ((1 << pcs) - 1)) == 0) wait_piece(lds, t2 >> pcs, lane);
+                    }
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kNBuf - 2) * kDmaPerWave + (kPfS ? 2 : 0)) : "memory");
+                    __builtin_amdgcn_s_barrier();
+                    if (dma_wave) dma_next_chunk(dma, dbuf);
+                    gather_stream(sb, sbt, cur, lane, mask, acc);
+                    load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
+                    pf_issue(cur);
+                    dbuf = dbuf == kNBuf - 1 ? 0 : dbuf + 1;
+                    if (prod_wave) produce_step(lds, wave, opaque_v(lane), false);
+                }
+                // units still in flight (a group whose gather ends first)
+                if (prod_wave)
+                    for (int i = 0; i < 3; ++i) produce_step(lds, wave, opaque_v(lane), true);
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            }
+        }
+
+        // ---- epilogue (k_stream's, HOW 0): park, re-read as rows, store ----
+        __syncthreads();
+        {
+            const int lane = opaque_v(threadIdx.x & 63);
+            const int wave = opaque_s(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+            const ItemPos q = item_pos(item);
+            const int g = q.cb * kWaves + wave;
+            cFusedArgs* F = fargs();
+            const bool active = g < F->G;
+            const int m0 = q.m0, z = q.z;
+            const int ncols = F->ncols, M = F->M, ldy = F->ldy;
+            const float a = F->a;
+            const float* Bias = F->Bias;
+            float* Y = F->Y;
+            float* ws = F->ws;
+            constexpr int kQ = kCW / 4;
+            constexpr int kStride = kCW * 4 + 16;
+            constexpr int kEpiRows = (kWaves * 128 * kStride <= kFusedStateOff) ? 128 : 64;
+            constexpr int kLanesPerPass = kEpiRows / 4;
+            constexpr int kRowsPerRead = 64 / kQ;
+            char* region = lds + wave * (kEpiRows * kStride);
+            const int col0 = group_col0(g);
+            const int col_end = min(col0 + wave_cols(wave), ncols);
+            const bool vec_ok = OUT == 0 ? ((ldy & 3) == 0 && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0))
+                                         : ((ncols & 3) == 0 && ((reinterpret_cast<uintptr_t>(ws) & 15) == 0));
+            constexpr bool kAddBias = OUT == 0 && !BIAS_FIRST;
+#pragma unroll
+            for (int h = 0; h < 256 / kEpiRows; ++h) {
+                if (active && lane / kLanesPerPass == h) {
+                    const int lh = lane % kLanesPerPass;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int R = 4 * lh + r;
+#pragma unroll
+                        for (int q = 0; q < kQ; ++q) {
+                            const float4 v = make_float4(acc_get(acc, 4 * (4 * q + 0) + r), acc_get(acc, 4 * (4 * q + 1) + r),
+                                                         acc_get(acc, 4 * (4 * q + 2) + r), acc_get(acc, 4 * (4 * q + 3) + r));
+                            *reinterpret_cast<float4*>(region + R * kStride + q * 16) = v;
+                        }
+                    }
+                }
+                __syncthreads();
+                if (active && lane < kRowsPerRead * kQ) {
+                    const int q = lane % kQ;
+                    const int col = col0 + 4 * q;
+                    float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (kAddBias) {
+                        bq.x = col + 0 < col_end ? Bias[col + 0] : 0.f;
+                        bq.y = col + 1 < col_end ? Bias[col + 1] : 0.f;
+                        bq.z = col + 2 < col_end ? Bias[col + 2] : 0.f;
+                        bq.w = col + 3 < col_end ? Bias[col + 3] : 0.f;
+                    }
+#pragma unroll 4
+                    for (int i = 0; i < (kEpiRows + kRowsPerRead - 1) / kRowsPerRead; ++i) {
+                        const int R = lane / kQ + kRowsPerRead * i;
+                        const int row = m0 + kEpiRows * h + R;
+                        if (R >= kEpiRows) break;
+                        float4 v = *reinterpret_cast<const float4*>(region + R * kStride + q * 16);
+                        if (row < M && col < col_end) {
+                            float* dst;
+                            if (OUT == 0) {
+                                dst = Y + (size_t)row * ldy + col;
+                                if (kAddBias) {
+                                    v.x += bq.x;
+                                    v.y += bq.y;
+                                    v.z += bq.z;
+                                    v.w += bq.w;
+                                }
+                                if (PRELU) {
+                                    v.x = (v.x < 0.0f) ? a * v.x : v.x;
+                                    v.y = (v.y < 0.0f) ? a * v.y : v.y;
+                                    v.z = (v.z < 0.0f) ? a * v.z : v.z;
+                                    v.w = (v.w < 0.0f) ? a * v.w : v.w;
+                                }
+                            } else {
+                                dst = ws + ((size_t)z * M + row) * ncols + col;
+                            }
+                            if (vec_ok && col + 3 < col_end) {
+                                if (OUT == 0) {
+                                    typedef float nt4 __attribute__((ext_vector_type(4)));
+                                    nt4 w = {v.x, v.y, v.z, v.w};
+                                    __builtin_nontemporal_store(w, reinterpret_cast<nt4*>(dst));
+                                } else {
+                                    *reinterpret_cast<float4*>(dst) = v;
+                                }
+                            } else {
+                                dst[0] = v.x;
+                                if (col + 1 < col_end) dst[1] = v.y;
+                                if (col + 2 < col_end) dst[2] = v.z;
+                                if (col + 3 < col_end) dst[3] = v.w;
+                            }
+                        }
+                    }
+                }
+                if (h + 1 < 256 / kEpiRows) __syncthreads();
+            }
+        }
+    }
+    // the last workgroup to finish advances the epoch (the counter wraps to 0)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned* sync = fargs()->sync;
+        const unsigned e = reinterpret_cast<const unsigned*>(lds + kFusedStateOff)[11];
+        if (atomicInc(sync + 1, gridDim.x - 1u) == gridDim.x - 1u)
+            __hip_atomic_store(sync, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // Split-K combine in slice order (deterministic): y = act(b + s0 + s1 ...)
 // or act(s0 + s1 + ... + b) depending on the variant's bias order.
 template <bool BIAS_FIRST, bool PRELU>
@@ -1144,10 +1690,73 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
     return hipGetLastError();
 }
 
+// The fused persistent launch (k_fused) of a whole call: X^T written by the
+// gather's own workgroups, split-K slabs reduced by k_reduce afterwards.
+template <bool BF, bool PR>
+static hipError_t launch_fused_t(const GemmArgs& g, int slices, hipStream_t st) {
+    const int nch = (g.K + kTK - 1) / kTK;
+    int cps = (nch + slices - 1) / slices;
+    slices = (nch + cps - 1) / cps;
+    FusedArgs A;
+    A.X = g.X;
+    A.XT = g.XT;
+    A.M = g.M;
+    A.K = g.K;
+    A.ldxt = ldxt_of(g.M);
+    A.ent = g.ent;
+    A.sptr = g.sptr;
+    A.n_entries = g.n_entries;
+    A.G = g.n_groups;
+    A.ncols = g.ncols;
+    A.nch = nch;
+    A.cps = cps;
+    A.Z = slices;
+    A.ncb = (g.n_groups + kWaves - 1) / kWaves;
+    A.n_items = ((g.M + kTM - 1) / kTM) * slices * A.ncb;
+    A.Bias = g.B;
+    A.Y = g.Y;
+    A.ldy = g.ldy;
+    A.a = g.a;
+    A.ws = g.ws;
+    pf_stream_params(g.n_entries, g.n_groups, nch, &A.pf_dist, &A.pf_lines);
+    A.sync = g.fsync;
+    A.pc = cps >= 128 ? 8 : cps >= 32 ? 4 : 2;
+    A.lead = env_int("TCSC_FUSED_LEAD", 2);
+    const int P = std::min(A.n_items, std::max(1, g.num_cus));
+    if (slices == 1)
+        hipLaunchKernelGGL((k_fused<BF, PR, 0>), dim3(P), dim3(kWaves * 64), 0, st, A);
+    else
+        hipLaunchKernelGGL((k_fused<BF, PR, 1>), dim3(P), dim3(kWaves * 64), 0, st, A);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || slices == 1) return e;
+    const long long total = (long long)g.M * g.ncols;
+    const bool vec = slices <= 16 && g.ncols % 4 == 0 && g.ldy % 4 == 0 &&
+                     ((reinterpret_cast<uintptr_t>(g.Y) | reinterpret_cast<uintptr_t>(g.ws) |
+                       reinterpret_cast<uintptr_t>(g.B)) & 15) == 0;
+    if (vec)
+        hipLaunchKernelGGL((k_reduce4<BF, PR>), dim3(grid_for(total / 4, 256)), dim3(256), 0, st,
+                           reinterpret_cast<const f32x4_t*>(g.ws), slices, g.M, g.ncols, g.B, g.Y, g.ldy, g.a);
+    else
+        hipLaunchKernelGGL((k_reduce<BF, PR>), dim3(grid_for(total, 256)), dim3(256), 0, st, g.ws, slices, g.M,
+                           g.ncols, g.B, g.Y, g.ldy, g.a);
+    return hipGetLastError();
+}
+
+bool fused_eligible(const GemmArgs& g) {
+    if (env_int("TCSC_FUSED", 0) == 0) return false;
+    return g.stage == 0 && g.fsync && g.order == 0 && g.num_cus > 0 && g.K >= kTK && g.K % 4 == 0 &&
+           ((reinterpret_cast<uintptr_t>(g.X) & 15) == 0) && (size_t)g.K * 4 * kTM < (1ull << 31);
+}
+
 // g.XT must hold xt_bytes(M, K) (the API layer carves it out of the plan's
 // workspace, ahead of the split-K slabs in g.ws).
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
     if (g.M <= 0 || g.ncols <= 0) return hipSuccess;
+    if (fused_eligible(g)) {
+        const int s = choose_slices(g.M, g.ncols, g.K, g.nnz, g.n_groups, g.ws ? g.ws_bytes : 0, g.force_slices);
+        if (g.bias_first) return g.prelu ? launch_fused_t<true, true>(g, s, st) : launch_fused_t<true, false>(g, s, st);
+        return g.prelu ? launch_fused_t<false, true>(g, s, st) : launch_fused_t<false, false>(g, s, st);
+    }
     if (g.K > 0 && g.stage != 2) {
         if (!g.XT) return hipErrorInvalidValue;
         const int ldxt = ldxt_of(g.M);

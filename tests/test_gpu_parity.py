@@ -520,8 +520,13 @@ def test_cfg4_eight_way_shards_full_size(gpu, torch_cuda, oracle, axis):
     rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
     rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
     tcsc_amd.gpu_from_dense(inp["Wd"], K, N, csp, csn, rip, rin)
-    del inp["Wd"]
     X, B = inp["X"], inp["B"]
+    # |b| + sum_{P u Q} |x| per element (the bound's scale): the dense product on magnitudes
+    S = torch.empty((M, N), device=dev)
+    Xa, Wa, Ba = X.abs(), inp.pop("Wd").abs_(), B.abs()
+    tcsc_amd.dense_sgemm(Xa, Wa, Ba, S, M, N, K, N, "basic", 0.0)
+    torch.cuda.synchronize()
+    del Xa, Wa, Ba
     Xi = torch.randint(-512, 513, (M, K), device=dev, dtype=torch.int32).float()
     Bi = B.round()
     full = tcsc_amd.Plan.from_device(K, N, csp, csn, rip, rin)
@@ -529,9 +534,6 @@ def test_cfg4_eight_way_shards_full_size(gpu, torch_cuda, oracle, axis):
     Y1, Y1i = torch.empty((M, N), device=dev), torch.empty((M, N), device=dev)
     full.sgemm(X, B, Y1, M, N, cfg.variant, 0.2)
     full.sgemm(Xi, Bi, Y1i, M, N, "basic", 0.0)
-    # |b| + sum |x| per element (the bound's scale), from the same gather on magnitudes
-    S = torch.empty((M, N), device=dev)
-    full.sgemm(X.abs(), B.abs(), S, M, N, "basic", 0.0)
     Yg, Ygi = torch.empty((M, N), device=dev), torch.empty((M, N), device=dev)
     for c0, c1 in all_ranges(N if axis == "cols" else M, G):
         if axis == "cols":
