@@ -72,8 +72,8 @@ struct tcsc_gpu_plan {
     size_t csc_bytes = 0;
     int mfma_min_M = 0;
     // the fused persistent gather's synchronisation block (tcsc::fused_sync_bytes
-    // for up to fsync_M rows; zeroed once, never reset: the counters carry
-    // the launch epoch) and the persistent grid size
+    // for up to fsync_M rows; zeroed once, then each launch zeroes the
+    // counter set the next launch uses) and the persistent grid size
     unsigned* fsync = nullptr;
     int fsync_M = 0;
     int num_cus = 0;
@@ -632,6 +632,7 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
     // the fused persistent kernel (tcsc::launch_gemm decides if it applies)
     if (ws == p->ws && p->fsync && M <= p->fsync_M) {
         g.fsync = p->fsync;
+        g.fsync_n = tcsc::fused_sync_pairs(p->fsync_M, p->rows);
         g.num_cus = p->num_cus;
     }
     // Bias first for tcsc_sgemm_basic (tcsc.c:74-96), last otherwise

@@ -176,24 +176,41 @@ static_assert(kTK % kUnitK == 0, "whole units per chunk");
 constexpr int kProdWave0 = 4;                    // producer waves 4, 5 (one LDS slot each)
 constexpr int kProdWaves = 2;
 constexpr int kPollWave = 6;                     // polls the piece counters
+static_assert(kProdWave0 >= kDmaWaves && kPollWave >= kDmaWaves, "producer and poll waves issue no ring DMAs");
 // LDS: the ring, one 256-B landing area that every wave's stream prefetch
 // shares (the data is never read), the producer slots, the item record
+#ifndef TCSC_FUSED_PF_LAST
+#define TCSC_FUSED_PF_LAST 0
+#endif
+constexpr int kFusedStateBytes = 128;  // item record (64 B) + producer states (16 B each) + 8 probe words
+constexpr int kProbeAhead = 4;         // chunks between a counter's probe and its check
+constexpr int kStoreDelay = 2;         // chunks from a unit's LDS-DMA to its stores
+constexpr int kSigDelay = 3;           // chunks from a unit's stores to its signal
+#if TCSC_FUSED_PF_LAST
+constexpr int kFusedSlotOff = kRingBytes;
+constexpr int kFusedStateOff = kFusedSlotOff + kProdWaves * kUnitBytes;
+constexpr int kFusedPfOff = kFusedStateOff + kFusedStateBytes;
+constexpr int kFusedLdsBytes0 = kFusedPfOff + 256;
+#else
 constexpr int kFusedPfOff = kRingBytes;
 constexpr int kFusedSlotOff = kFusedPfOff + 256;
 constexpr int kFusedStateOff = kFusedSlotOff + kProdWaves * kUnitBytes;
-constexpr int kFusedStateBytes = 128;  // item record (64 B) + producer states (16 B each)
 constexpr int kFusedLdsBytes0 = kFusedStateOff + kFusedStateBytes;
+#endif
+constexpr int kFusedProbeOff = kFusedStateOff + 96;
 constexpr int kFusedLdsBytes = kFusedLdsBytes0 > kEpiMinBytes ? kFusedLdsBytes0 : kEpiMinBytes;
 static_assert(kFusedLdsBytes <= 160 * 1024, "fused kernel LDS");
 // synchronisation block of a plan (device memory, zeroed once): [0] the
 // epoch of the last completed launch, [1] arrivals of the running launch,
-// then 64-bit piece counters, one per (row tile, chunk) of the largest
-// launch the block was sized for
+// then per (row tile, chunk) of the largest launch the block was sized for
+// two 32-bit piece counters, one per epoch parity (a launch counts on its
+// own set and zeroes the other for the next launch)
 constexpr size_t kFusedSyncHdr = 256;
-inline size_t fused_sync_bytes(int M, int K) {
-    const size_t nrt = (size_t)(M + kTM - 1) / kTM, nch = (size_t)(K + kTK - 1) / kTK;
-    return kFusedSyncHdr + nrt * (nch > 0 ? nch : 1) * 8;
+inline int fused_sync_pairs(int M, int K) {
+    const int nrt = (M + kTM - 1) / kTM, nch = (K + kTK - 1) / kTK;
+    return nrt * (nch > 0 ? nch : 1);
 }
+inline size_t fused_sync_bytes(int M, int K) { return kFusedSyncHdr + (size_t)fused_sync_pairs(M, K) * 8; }
 
 struct FusedArgs {
     const float* X = nullptr;       // M x K row-major
@@ -211,7 +228,8 @@ struct FusedArgs {
     int pf_dist = 0, pf_lines = 1;
     unsigned* sync = nullptr;       // fused_sync_bytes(M, K) block
     int pc = 8;                     // chunks per piece
-    int lead = 2;                   // pieces produced before an item's gather starts
+    int lead = 2;                   // pieces produced before an item's gather starts (~16 chunks' worth)
+    int sync_n = 0;                 // (row tile, chunk) counter pairs in the sync block
 };
 
 struct GemmArgs {
@@ -243,6 +261,7 @@ struct GemmArgs {
     // stage 0 only: the plan's synchronisation block (fused_sync_bytes for at
     // least this M) enables the fused persistent kernel; null = k_transpose + k_stream
     unsigned* fsync = nullptr;
+    int fsync_n = 0;           // counter pairs in fsync (fused_sync_pairs of the size it was made for)
     int num_cus = 0;           // persistent grid size (workgroups, one per CU)
 };
 

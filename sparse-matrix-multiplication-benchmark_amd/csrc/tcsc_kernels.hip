@@ -806,27 +806,62 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
 // resident: the GPU shared with another kernel) makes the waiting workgroup
 // produce the piece itself (the same values; writes are idempotent).
 constexpr int kPollLimit = 1 << 12;
+#ifndef TCSC_FUSED_DIAG_PURE  // timing diagnostic only (tools/ab.mk fpu): k_transpose first, no production or polls
+#define TCSC_FUSED_DIAG_PURE 0
+#endif
+#ifndef TCSC_FUSED_DIAG_NOLOOP  // timing diagnostic only (tools/ab.mk fnl): no in-loop production or polls
+#define TCSC_FUSED_DIAG_NOLOOP TCSC_FUSED_DIAG_PURE
+#endif
+// Timing diagnostic (tools/ab.mk fst, tools/fused_stamps.py): per workgroup,
+// s_memtime cycles of each item phase, of the producer steps that act, of
+// the poll wave's in-loop checks and of wave 0's chunk-barrier waits,
+// accumulated in LDS and added to g_fstamp at the end.
+#ifndef TCSC_FUSED_STAMPS
+#define TCSC_FUSED_STAMPS 0
+#endif
+#if TCSC_FUSED_STAMPS
+__device__ unsigned long long g_fstamp[4096 * 8];
+#define FST_NOW() ((unsigned long long)__builtin_amdgcn_s_memtime())
+#define FST_ADD(lds, slot, v)                                                                        \
+    do {                                                                                             \
+        if ((threadIdx.x & 63) == 0)                                                                 \
+            __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>((lds) + kFusedLdsBytes0) + (slot), \
+                                   (unsigned long long)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+    } while (0)
+#else
+#define FST_NOW() 0ull
+#define FST_ADD(lds, slot, v) \
+    do {                      \
+    } while (0)
+#endif
 
 __device__ __forceinline__ int xcd_slot(int b, int P) {
     const int q = P >> 3, r = P & 7, x = b & 7;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
 }
 
-__device__ __forceinline__ void piece_signal(unsigned long long* c, unsigned e) {
-    unsigned long long v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (;;) {
-        const unsigned long long nv = (unsigned)(v >> 32) == e ? v + 1ull : (((unsigned long long)e << 32) | 1ull);
-        if (__hip_atomic_compare_exchange_strong(c, &v, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT))
-            return;
-    }
+// Piece counters: 32-bit, two sets used by alternate launches (epoch
+// parity); a launch zeroes the other set for the next one, so a signal is a
+// plain atomic add (no compare-and-swap retries among a piece's ~100 agents).
+__device__ __forceinline__ void piece_signal(unsigned* c) {
+    (void)__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ bool piece_ready(unsigned long long* c, unsigned e, unsigned tgt) {
-    const unsigned long long v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-    return hi == e && lo >= tgt;
+__device__ __forceinline__ bool piece_ready(unsigned* c, unsigned tgt) {
+    const unsigned v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (unsigned)__builtin_amdgcn_readfirstlane((int)v) >= tgt;
+}
+
+// Early probe of a piece counter (poll wave, a few chunks before the piece
+// is needed): one lane's sc1 LDS-DMA of the counter into an LDS word, so the
+// round trip overlaps the gather instead of stalling the chunk barrier.
+__device__ __forceinline__ void piece_probe(unsigned ldsw, const unsigned* c) {
+    unsigned sv;
+    asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %[m]\n\ts_nop 0\n\tglobal_load_lds_dword %[o], %[b] sc1\n\t"
+                 "s_mov_b32 m0, %[sv]"
+                 : [sv] "=&s"(sv)
+                 : [m] "s"(ldsw), [o] "v"(0u), [b] "s"(c)
+                 : "memory");
 }
 
 // LDS-DMA of unit (X rows m0 .. m0+255, k0 .. k0+3) into LDS at `slot`:
@@ -838,11 +873,14 @@ __device__ __forceinline__ void unit_dma(const float* X, int K, int M, int m0, i
 #pragma unroll
     for (int r = 0; r < 4; ++r) off[r] = (unsigned)min(4 * lane + r, mmax) * (unsigned)K * 4u;
     unsigned sv;
+#ifndef TCSC_UNIT_NOP
+#define TCSC_UNIT_NOP "0"
+#endif
     asm volatile("s_mov_b32 %[sv], m0\n\t"
-                 "s_mov_b32 m0, %[s0]\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o0], %[b]\n\t"
-                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o1], %[b]\n\t"
-                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o2], %[b]\n\t"
-                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o3], %[b]\n\t"
+                 "s_mov_b32 m0, %[s0]\n\ts_nop " TCSC_UNIT_NOP "\n\tglobal_load_lds_dwordx4 %[o0], %[b]\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop " TCSC_UNIT_NOP "\n\tglobal_load_lds_dwordx4 %[o1], %[b]\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop " TCSC_UNIT_NOP "\n\tglobal_load_lds_dwordx4 %[o2], %[b]\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop " TCSC_UNIT_NOP "\n\tglobal_load_lds_dwordx4 %[o3], %[b]\n\t"
                  "s_mov_b32 m0, %[sv]"
                  : [sv] "=&s"(sv)
                  : [s0] "s"(slot), [o0] "v"(off[0]), [o1] "v"(off[1]), [o2] "v"(off[2]), [o3] "v"(off[3]),
@@ -851,6 +889,23 @@ __device__ __forceinline__ void unit_dma(const float* X, int K, int M, int m0, i
 }
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// Four global_store_dwordx4 sc1 (rows o, o+st, o+2st, o+3st of base) in one
+// asm block.  A store of more than 8 bytes still reads its data VGPRs in the
+// cycle after issue: a VALU write to them right after it corrupts the value
+// the last quarter-wave stores (the compiler's hazard recognizer does not
+// see stores inside inline asm), hence the trailing s_nop.
+__device__ __forceinline__ void store4_sc1(char* base, unsigned o, unsigned st, f32x4v r0, f32x4v r1, f32x4v r2,
+                                           f32x4v r3) {
+    asm volatile("global_store_dwordx4 %0, %4, %8 sc1\n\t"
+                 "global_store_dwordx4 %1, %5, %8 sc1\n\t"
+                 "global_store_dwordx4 %2, %6, %8 sc1\n\t"
+                 "global_store_dwordx4 %3, %7, %8 sc1\n\t"
+                 "s_nop 1"
+                 ::"v"(o), "v"(o + st), "v"(o + 2 * st), "v"(o + 3 * st), "v"(r0), "v"(r1), "v"(r2), "v"(r3),
+                   "s"(base)
+                 : "memory");
+}
 
 // X^T rows k0 .. k0+3, columns m0 .. m0+255 from the unit staged at lds + slot
 // (ds_read_b128 x 4, the 4 x 4 block of lane l transposed in registers,
@@ -863,10 +918,7 @@ __device__ __forceinline__ void unit_store(const char* lds_slot, float* XT, int 
     const unsigned o = 16u * lane, st = (unsigned)ldxt * 4u;
     const f32x4v r0 = {x0.x, x1.x, x2.x, x3.x}, r1 = {x0.y, x1.y, x2.y, x3.y};
     const f32x4v r2 = {x0.z, x1.z, x2.z, x3.z}, r3 = {x0.w, x1.w, x2.w, x3.w};
-    asm volatile("global_store_dwordx4 %0, %1, %2 sc1" ::"v"(o), "v"(r0), "s"(base) : "memory");
-    asm volatile("global_store_dwordx4 %0, %1, %2 sc1" ::"v"(o + st), "v"(r1), "s"(base) : "memory");
-    asm volatile("global_store_dwordx4 %0, %1, %2 sc1" ::"v"(o + 2 * st), "v"(r2), "s"(base) : "memory");
-    asm volatile("global_store_dwordx4 %0, %1, %2 sc1" ::"v"(o + 3 * st), "v"(r3), "s"(base) : "memory");
+    store4_sc1(base, o, st, r0, r1, r2, r3);
 }
 
 // The same unit through registers (the timeout path: one wave, no LDS).
@@ -879,11 +931,9 @@ __device__ __forceinline__ void unit_direct(const float* X, int K, int M, float*
         x[r] = *reinterpret_cast<const f32x4v*>(X + (size_t)(m0 + min(4 * lane + r, mmax)) * K + k0);
     char* base = reinterpret_cast<char*>(XT + (size_t)k0 * ldxt + m0);
     const unsigned o = 16u * lane, st = (unsigned)ldxt * 4u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const f32x4v v = {x[0][j], x[1][j], x[2][j], x[3][j]};
-        asm volatile("global_store_dwordx4 %0, %1, %2 sc1" ::"v"(o + j * st), "v"(v), "s"(base) : "memory");
-    }
+    const f32x4v r0 = {x[0].x, x[1].x, x[2].x, x[3].x}, r1 = {x[0].y, x[1].y, x[2].y, x[3].y};
+    const f32x4v r2 = {x[0].z, x[1].z, x[2].z, x[3].z}, r3 = {x[0].w, x[1].w, x[2].w, x[3].w};
+    store4_sc1(base, o, st, r0, r1, r2, r3);
 }
 
 // The kernel's arguments, re-read from the kernarg segment at each use
@@ -901,7 +951,7 @@ __device__ __forceinline__ cFusedArgs* fargs() {
 // producer and poll waves inside the chunk loop, so none of it is live in
 // registers across the gather): dwords
 //   0-1 X + m0*K (bytes)   2-3 XT + m0 (bytes)   4 K   5 M-1-m0   6 ldxt   7 k_lo
-//   8 U (units)   9 units per piece   10 An (agents)   11 epoch   12 log2(pc)   13 chunks
+//   8 U (units)   9 units per piece   10 An (agents)   11 epoch   12 log2(pc)   13 lead
 //   14-15 the counter of piece 0
 // Producer state (waves 4, 5), dwords: 0 next unit (INT_MAX: none left),
 // 1 unit in the slot (-1: none), 2 unit whose stores were issued last (-1).
@@ -909,8 +959,8 @@ struct ItemRec {
     unsigned long long xrow, xtrow;
     int K, mmax, ldxt, k_lo, U, upc, An;
     unsigned e;
-    int pcs, nloc;  // log2(chunks per piece), chunks of the item
-    unsigned long long crow;
+    int pcs, lead;  // log2(chunks per piece), pieces produced in the item prologue
+    unsigned long long crow;  // this launch's counter of piece 0 (stride 2 words per chunk)
 };
 static_assert(sizeof(ItemRec) == 64, "item record layout");
 
@@ -931,62 +981,99 @@ __device__ __forceinline__ ItemRec load_rec(const char* lds) {
     r.An = __builtin_amdgcn_readfirstlane(c.z);
     r.e = (unsigned)__builtin_amdgcn_readfirstlane(c.w);
     r.pcs = __builtin_amdgcn_readfirstlane(d.x);
-    r.nloc = __builtin_amdgcn_readfirstlane(d.y);
+    r.lead = __builtin_amdgcn_readfirstlane(d.y);
     r.crow = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(d.w) << 32) |
              (unsigned)__builtin_amdgcn_readfirstlane(d.z);
     return r;
 }
 
-// One production step of a producer wave: the unit issued last time lands
-// (its LDS-DMA had a chunk of gather to arrive), is transposed and stored;
-// the stores issued last time are complete, so their piece is signalled if
-// they were this agent's last units of it; the next unit's DMA is issued.
-// `drain` waits for everything (the flush after the chunk loop).
-__device__ __forceinline__ void produce_step(char* lds, int wave, int lane, bool drain) {
+// One production step of a producer wave, at chunk t of the item (relative
+// to its first chunk).  An agent's units move through three stages, one unit
+// per stage at a time (producer state in LDS: next unit, the unit in the LDS
+// slot and when its DMA was issued, the unit stored and when):
+//   DMA: unit u of piece p is issued once t >= (p - lead) * pc, i.e. about
+//        lead pieces ahead of the chunk that polls p -- production keeps a
+//        fixed distance ahead of the gather instead of racing it (racing
+//        makes every producer wave wait on its own stores each chunk, and the
+//        barrier makes the whole workgroup wait with it);
+//   store: kStoreDelay chunks later (an LDS-DMA from HBM takes ~1.1 us to
+//        land, more than a chunk), transposed and stored;
+//   signal: kSigDelay chunks after the stores, which have completed by then,
+//        so the s_waitcnt costs nothing; the piece's counter is bumped when
+//        this was the agent's last unit of the piece.
+// `drain` (after the chunk loop) moves every stage at once.  Returns the
+// next chunk at which a stage can move (the caller skips the step until
+// then: no LDS read per chunk), INT_MAX once the wave has nothing left.
+__device__ __forceinline__ int produce_step(char* lds, int wave, int lane, int t, bool drain) {
     int4* stp = reinterpret_cast<int4*>(lds + kFusedStateOff + 64) + (wave - kProdWave0);
     const int4 st = *stp;
-    int u_next = __builtin_amdgcn_readfirstlane(st.x), slot_u = __builtin_amdgcn_readfirstlane(st.y),
-        sig_u = __builtin_amdgcn_readfirstlane(st.z);
-    if (u_next == 0x7fffffff && slot_u < 0 && sig_u < 0) return;
+    int u_next = __builtin_amdgcn_readfirstlane(st.x), d_u = __builtin_amdgcn_readfirstlane(st.y),
+        s_u = __builtin_amdgcn_readfirstlane(st.z);
+    const int tw = __builtin_amdgcn_readfirstlane(st.w);
+    if (u_next == 0x7fffffff && d_u < 0 && s_u < 0) return 0x7fffffff;
+    int tD = tw & 0xffff, tS = (tw >> 16) & 0xffff;
     const ItemRec r = load_rec(lds);
+    const bool sig_now = s_u >= 0 && (drain || t >= tS + kSigDelay);
+    const bool store_now = d_u >= 0 && (s_u < 0 || sig_now) && (drain || t >= tD + kStoreDelay);
+    const bool dma_now = (d_u < 0 || store_now) && u_next < r.U &&
+                         (drain || t >= ((u_next / r.upc - r.lead) << r.pcs));
+    // the next chunk at which a stage can move
+    auto next_t = [&]() {
+        int tn = 0x7fffffff;
+        if (s_u >= 0) tn = min(tn, tS + kSigDelay);
+        if (d_u >= 0) tn = min(tn, tD + kStoreDelay);
+        else if (u_next < r.U) tn = min(tn, (u_next / r.upc - r.lead) << r.pcs);
+        return max(tn, t + 1);
+    };
+    if (!sig_now && !store_now && !dma_now) return next_t();
+    // everything but the stream prefetch issued at the end of the last chunk
+    // (issued after every unit DMA and store of this wave): the DMA/stores
+    // waited for are >= kStoreDelay-1 chunks old and have landed
     if (drain)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else  // all but this chunk's stream prefetch
-        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    unsigned long long* crow = reinterpret_cast<unsigned long long*>(r.crow);
-    if (sig_u >= 0) {
-        const int p = sig_u / r.upc;
-        if (sig_u + r.An >= min(r.U, (p + 1) * r.upc) && lane == 0) piece_signal(crow + ((size_t)p << r.pcs), r.e);
-        sig_u = -1;
+    else if (sig_now || store_now)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPfS ? 1 : 0) : "memory");
+    if (sig_now) {
+        const int p = s_u / r.upc;
+        unsigned* crow = reinterpret_cast<unsigned*>(r.crow);
+        if (s_u + r.An >= min(r.U, (p + 1) * r.upc) && lane == 0) piece_signal(crow + ((size_t)p << (r.pcs + 1)));
+        s_u = -1;
     }
-    const float* X = reinterpret_cast<const float*>(r.xrow);
-    float* XT = reinterpret_cast<float*>(r.xtrow);
     const char* slot_ptr = lds + kFusedSlotOff + (wave - kProdWave0) * kUnitBytes;
-    if (slot_u >= 0) {
-        unit_store(slot_ptr, XT + (size_t)(r.k_lo + kUnitK * slot_u) * r.ldxt, r.ldxt, 0, 0, lane);
-        sig_u = slot_u;
-        slot_u = -1;
+    if (store_now) {
+        float* XT = reinterpret_cast<float*>(r.xtrow);
+        unit_store(slot_ptr, XT + (size_t)(r.k_lo + kUnitK * d_u) * r.ldxt, r.ldxt, 0, 0, lane);
+        s_u = d_u;
+        tS = t;
+        d_u = -1;
     }
-    if (u_next < r.U) {
+    if (dma_now) {
+        const float* X = reinterpret_cast<const float*>(r.xrow);
         unit_dma(X + r.k_lo + kUnitK * u_next, r.K, r.mmax + 1, 0, 0,
                  (unsigned)reinterpret_cast<uintptr_t>(slot_ptr), lane);
-        slot_u = u_next;
+        d_u = u_next;
+        tD = t;
         u_next = u_next + r.An < r.U ? u_next + r.An : 0x7fffffff;
-    } else {
-        u_next = 0x7fffffff;
     }
-    if (lane == 0) *stp = make_int4(u_next, slot_u, sig_u, 0);
+    if (lane == 0) *stp = make_int4(u_next, d_u, s_u, (tS << 16) | tD);
+    if (u_next == 0x7fffffff && d_u < 0 && s_u < 0) return 0x7fffffff;
+    return next_t();
 }
 
 // Wave 6 before the barrier ahead of chunk c+kNBuf-1's DMA: when that chunk
 // opens a piece, wait until the piece's counter is complete.  Past
 // kPollLimit polls (a member that is not running) the wave writes the
 // piece's X^T rows itself.
-__device__ __forceinline__ void wait_piece(const char* lds, int p, int lane) {
+__device__ __forceinline__ void wait_piece(const char* lds, int p, int lane, bool probed) {
     const ItemRec r = load_rec(lds);
-    unsigned long long* c = reinterpret_cast<unsigned long long*>(r.crow) + ((size_t)p << r.pcs);
+    unsigned* c = reinterpret_cast<unsigned*>(r.crow) + ((size_t)p << (r.pcs + 1));
     const unsigned tgt = (unsigned)min(r.An, min(r.U, (p + 1) * r.upc) - p * r.upc);
-    for (int n = 0; !piece_ready(c, r.e, tgt); ++n) {
+    if (probed) {  // the probe issued kProbeAhead chunks ago (all but the last stream prefetch are done)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPfS ? 1 : 0) : "memory");
+        const unsigned v = reinterpret_cast<const volatile unsigned*>(lds + kFusedProbeOff)[p & 7];
+        if ((unsigned)__builtin_amdgcn_readfirstlane((int)v) >= tgt) return;
+    }
+    for (int n = 0; !piece_ready(c, tgt); ++n) {
         if (n > kPollLimit) {
             const float* X = reinterpret_cast<const float*>(r.xrow);
             float* XT = reinterpret_cast<float*>(r.xtrow);
@@ -999,6 +1086,17 @@ __device__ __forceinline__ void wait_piece(const char* lds, int p, int lane) {
         }
         __builtin_amdgcn_s_sleep(2);
     }
+}
+
+// Poll wave, kProbeAhead chunks before the check of piece p: the probe of
+// its counter.
+__device__ __forceinline__ void probe_issue(const char* lds, int p, int pcs, int lane) {
+    const int* rec = reinterpret_cast<const int*>(lds + kFusedStateOff);
+    const unsigned long long cr = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(rec[15]) << 32) |
+                                  (unsigned)__builtin_amdgcn_readfirstlane(rec[14]);
+    const unsigned* c = reinterpret_cast<const unsigned*>(cr) + ((size_t)p << (pcs + 1));
+    if (lane == 0)
+        piece_probe((unsigned)reinterpret_cast<uintptr_t>(lds) + kFusedProbeOff + 4u * (unsigned)(p & 7), c);
 }
 
 // Opaque copies: the value is the same, but the compiler cannot hoist what
@@ -1033,18 +1131,29 @@ __device__ __forceinline__ ItemPos item_pos(int item) {
 
 template <bool BIAS_FIRST, bool PRELU, int OUT>
 __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const FusedArgs A) {
-    __shared__ __attribute__((aligned(16))) char lds[kFusedLdsBytes];
+    __shared__ __attribute__((aligned(16))) char lds[kFusedLdsBytes + (TCSC_FUSED_STAMPS ? 64 : 0)];
     (void)A;  // every field is read through fargs()
+#if TCSC_FUSED_STAMPS
+    if (threadIdx.x < 8) reinterpret_cast<unsigned long long*>(lds + kFusedLdsBytes0)[threadIdx.x] = 0;
+    __syncthreads();
+#endif
     {
         // the epoch of this launch: the last completed launch's + 1
         unsigned* sync = fargs()->sync;
         const unsigned e = (unsigned)__builtin_amdgcn_readfirstlane(
             (int)(__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u));
         if (threadIdx.x == 0) reinterpret_cast<unsigned*>(lds + kFusedStateOff)[11] = e;
+        // zero the other set of piece counters for the next launch (this
+        // launch uses set e & 1 only; the kernel boundary orders the stores)
+        unsigned* cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(sync) + kFusedSyncHdr) + (~e & 1u);
+        const int n = fargs()->sync_n;
+        for (int i = blockIdx.x * (int)blockDim.x + (int)threadIdx.x; i < n; i += (int)(gridDim.x * blockDim.x))
+            cnt[2 * (size_t)i] = 0u;
     }
 
     for (int item = xcd_slot(blockIdx.x, gridDim.x); item < fargs()->n_items; item = opaque_s(item + (int)gridDim.x)) {
         // ---- item prologue: this agent's units of the first `lead` pieces, the record, piece 0 ----
+        const unsigned long long fst0 = FST_NOW();
         {
             const int lane = opaque_v(threadIdx.x & 63);
             const int wave = opaque_s(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
@@ -1061,19 +1170,19 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
             const int U = q.c_begin < q.c_end ? (min(q.c_end * kTK, K) - k_lo + kUnitK - 1) / kUnitK : 0;
             const int pc = F->pc, upc = kUnitsPerChunk * pc;
             const int npieces = (U + upc - 1) / upc;
-            // every piece up front when the members cannot keep ahead (one unit
-            // per chunk and agent against the group's 12 units per chunk)
-            const int lead = (An * 10 < kUnitsPerChunk * 11) ? npieces : min(F->lead, npieces);
-            const int agent = (item < mem_end && prod_wave) ? kProdWaves * (item - gi0) + (wave - kProdWave0) : -1;
-            unsigned long long* const crow =
-                reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(F->sync) + kFusedSyncHdr) +
-                (size_t)q.rt * nch + q.c_begin;
+            // every piece up front when the members cannot keep ahead (an agent
+            // moves a unit every kSigDelay chunks at most; the group needs 12 per chunk)
+            const int lead = (An < kSigDelay * kUnitsPerChunk + 4) ? npieces : min(F->lead, npieces);
+            const int agent = (!TCSC_FUSED_DIAG_PURE && item < mem_end && prod_wave) ? kProdWaves * (item - gi0) + (wave - kProdWave0) : -1;
+            unsigned* const crow0 = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(F->sync) + kFusedSyncHdr) +
+                                    2 * ((size_t)q.rt * nch + q.c_begin);
             const float* Xr = F->X + (size_t)q.m0 * K;
             float* XTr = F->XT + q.m0;
             const int ldxt = F->ldxt;
             __syncthreads();  // the previous item's epilogue is done with the LDS
             int4* rec4 = reinterpret_cast<int4*>(lds + kFusedStateOff);
             const unsigned e = (unsigned)__builtin_amdgcn_readfirstlane(rec4[2].w);
+            unsigned* const crow = crow0 + (e & 1u);  // this launch's set
             int u_next = agent;
             if (agent >= 0) {
                 const int lead_units = min(U, lead * upc);
@@ -1093,7 +1202,7 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
                 if (lane == 0)
                     for (int p = 0; p < lead; ++p) {
                         const int f = p * upc + (((agent - p * upc) % An) + An) % An;  // the agent's first unit in p
-                        if (f < min(U, (p + 1) * upc)) piece_signal(crow + (size_t)p * pc, e);
+                        if (f < min(U, (p + 1) * upc)) piece_signal(crow + 2 * (size_t)p * pc);
                     }
             }
             if (prod_wave && lane == 0)
@@ -1106,12 +1215,14 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
                 rec4[0] = make_int4((int)xr, (int)(xr >> 32), (int)xtr, (int)(xtr >> 32));
                 rec4[1] = make_int4(K, M - 1 - q.m0, ldxt, k_lo);
                 rec4[2] = make_int4(U, upc, An, (int)e);
-                rec4[3] = make_int4(31 - __builtin_clz(pc), q.c_end - q.c_begin, (int)cr, (int)(cr >> 32));
+                rec4[3] = make_int4(31 - __builtin_clz(pc), lead, (int)cr, (int)(cr >> 32));
             }
             __syncthreads();  // the record, before the first wait
-            if (wave == kPollWave && npieces > 0) wait_piece(lds, 0, lane);
+            if (!TCSC_FUSED_DIAG_PURE && wave == kPollWave && npieces > 0) wait_piece(lds, 0, lane, false);
             __syncthreads();
         }
+        const unsigned long long fst1 = FST_NOW();
+        if (threadIdx.x < 64) FST_ADD(lds, 0, fst1 - fst0);
 
         facc_t acc[TCSC_ACC_VECS];
 #pragma unroll
@@ -1182,31 +1293,55 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 const unsigned mask = 0x3ffu;
                 int dbuf = (buf0 + kNBuf - 1) % kNBuf;
+                // per-wave event state in SGPRs (no LDS read per chunk): log2(pc)
+                // for the poll wave, the next chunk a producer wave can act at
+                const int pcs = opaque_s(__builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(lds + kFusedStateOff)[12]));
+                int t_evt = 0;
                 for (int c = c_begin; c < c_end; ++c) {
-                    if (wave == kPollWave) {  // chunk c+kNBuf-1 is DMA'd right after this barrier
-                        const int* rec = reinterpret_cast<const int*>(lds + kFusedStateOff);
-                        const int pcs = __builtin_amdgcn_readfirstlane(rec[12]);  // log2(pc)
+                    if (!TCSC_FUSED_DIAG_NOLOOP && wave == kPollWave) {  // chunk c+kNBuf-1 is DMA'd right after this barrier
                         const int t2 = c + kNBuf - 1 - c_begin;
-                        if (t2 < c_end - c_begin && (t2 & ((1 << pcs) - 1)) == 0) wait_piece(lds, t2 >> pcs, lane);
+                        if (t2 < c_end - c_begin && (t2 & ((1 << pcs) - 1)) == 0) {
+                            const unsigned long long w0 = FST_NOW();
+                            wait_piece(lds, t2 >> pcs, lane, t2 >= kNBuf - 1 + kProbeAhead);
+                            FST_ADD(lds, 4, FST_NOW() - w0);
+                        }
                     }
+#if TCSC_FUSED_STAMPS
+                    const unsigned long long b0 = FST_NOW();
+#endif
                     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kNBuf - 2) * kDmaPerWave + (kPfS ? 2 : 0)) : "memory");
                     __builtin_amdgcn_s_barrier();
+#if TCSC_FUSED_STAMPS
+                    if (wave == 0) FST_ADD(lds, 6, FST_NOW() - b0);
+#endif
                     if (dma_wave) dma_next_chunk(dma, dbuf);
                     gather_stream(sb, sbt, cur, lane, mask, acc);
                     load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
+                    if (!TCSC_FUSED_DIAG_NOLOOP && prod_wave && c - c_begin >= t_evt) {
+                        const unsigned long long p0 = FST_NOW();
+                        t_evt = produce_step(lds, wave, opaque_v(lane), c - c_begin, false);
+                        FST_ADD(lds, 3, FST_NOW() - p0);
+                        FST_ADD(lds, 7, 1);
+                    }
+                    if (!TCSC_FUSED_DIAG_NOLOOP && wave == kPollWave) {  // probe the counter this wave checks kProbeAhead chunks from now
+                        const int t3 = c + kNBuf - 1 + kProbeAhead - c_begin;
+                        if (t3 < c_end - c_begin && (t3 & ((1 << pcs) - 1)) == 0) probe_issue(lds, t3 >> pcs, pcs, opaque_v(lane));
+                    }
                     pf_issue(cur);
                     dbuf = dbuf == kNBuf - 1 ? 0 : dbuf + 1;
-                    if (prod_wave) produce_step(lds, wave, opaque_v(lane), false);
                 }
                 // units still in flight (a group whose gather ends first)
                 if (prod_wave)
-                    for (int i = 0; i < 3; ++i) produce_step(lds, wave, opaque_v(lane), true);
+                    while (produce_step(lds, wave, opaque_v(lane), 0xffff, true) != 0x7fffffff) {
+                    }
                 asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             }
         }
 
         // ---- epilogue (k_stream's, HOW 0): park, re-read as rows, store ----
         __syncthreads();
+        const unsigned long long fst2 = FST_NOW();
+        if (threadIdx.x < 64) FST_ADD(lds, 1, fst2 - fst1);
         {
             const int lane = opaque_v(threadIdx.x & 63);
             const int wave = opaque_s(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
@@ -1302,9 +1437,15 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
                 if (h + 1 < 256 / kEpiRows) __syncthreads();
             }
         }
+        if (threadIdx.x < 64) FST_ADD(lds, 2, FST_NOW() - fst2);
     }
     // the last workgroup to finish advances the epoch (the counter wraps to 0)
     __syncthreads();
+#if TCSC_FUSED_STAMPS
+    if (threadIdx.x < 8)
+        atomicAdd(&g_fstamp[(blockIdx.x & 4095) * 8 + threadIdx.x],
+                  reinterpret_cast<const unsigned long long*>(lds + kFusedLdsBytes0)[threadIdx.x]);
+#endif
     if (threadIdx.x == 0) {
         unsigned* sync = fargs()->sync;
         const unsigned e = reinterpret_cast<const unsigned*>(lds + kFusedStateOff)[11];
@@ -1695,6 +1836,10 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
 template <bool BF, bool PR>
 static hipError_t launch_fused_t(const GemmArgs& g, int slices, hipStream_t st) {
     const int nch = (g.K + kTK - 1) / kTK;
+#if TCSC_FUSED_DIAG_PURE
+    hipLaunchKernelGGL(k_transpose<true>, dim3((g.K + 127) / 128, ldxt_of(g.M) / 64), dim3(256), 0, st, g.X, g.M, g.K,
+                       g.XT, ldxt_of(g.M));
+#endif
     int cps = (nch + slices - 1) / slices;
     slices = (nch + cps - 1) / cps;
     FusedArgs A;
@@ -1720,8 +1865,11 @@ static hipError_t launch_fused_t(const GemmArgs& g, int slices, hipStream_t st) 
     A.ws = g.ws;
     pf_stream_params(g.n_entries, g.n_groups, nch, &A.pf_dist, &A.pf_lines);
     A.sync = g.fsync;
+    A.sync_n = g.fsync_n;
     A.pc = cps >= 128 ? 8 : cps >= 32 ? 4 : 2;
-    A.lead = env_int("TCSC_FUSED_LEAD", 2);
+    // pieces produced in an item's prologue: ~16 chunks' worth, so in-loop
+    // production starts 16 chunks ahead of the poll of the piece it feeds
+    A.lead = env_int("TCSC_FUSED_LEAD", (16 + A.pc - 1) / A.pc);
     const int P = std::min(A.n_items, std::max(1, g.num_cus));
     if (slices == 1)
         hipLaunchKernelGGL((k_fused<BF, PR, 0>), dim3(P), dim3(kWaves * 64), 0, st, A);
@@ -1741,6 +1889,16 @@ static hipError_t launch_fused_t(const GemmArgs& g, int slices, hipStream_t st) 
                            g.ncols, g.B, g.Y, g.ldy, g.a);
     return hipGetLastError();
 }
+
+#if TCSC_FUSED_STAMPS
+}  // namespace tcsc
+extern "C" int tcsc_diag_fused_stamps(unsigned long long* out, int n) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tcsc::g_fstamp), (size_t)n * 8) != hipSuccess) return -1;
+    static unsigned long long zero[4096 * 8];
+    return hipMemcpyToSymbol(HIP_SYMBOL(tcsc::g_fstamp), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+namespace tcsc {
+#endif
 
 bool fused_eligible(const GemmArgs& g) {
     if (env_int("TCSC_FUSED", 0) == 0) return false;

@@ -99,3 +99,18 @@ lib/abl/libtcsc_amd_pfs%.so: $(SRC)/tcsc_kernels.hip $(SRC)/tcsc_api.cpp $(OBJ)/
 	$(HIPCC) $(HIPFLAGS) -DTCSC_PF_S=$* -c $(SRC)/tcsc_kernels.hip -o $(OBJ)/abl/k_pfs$*.o
 	$(HIPCC) $(HIPFLAGS) -DTCSC_PF_S=$* -c $(SRC)/tcsc_api.cpp -o $(OBJ)/abl/a_pfs$*.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)/abl/k_pfs$*.o $(OBJ)/abl/a_pfs$*.o $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o -lpthread -L$(ROCM)/lib -lrocblas -Wl,-rpath,$(ROCM)/lib
+
+# fused-kernel diagnostics: lib/abl/libtcsc_amd_fpf.so (stream-prefetch landing area after the
+# producer slots), lib/abl/libtcsc_amd_fnop.so (s_nop 4 after every M0 write of a unit's LDS-DMA)
+FDEF_pf := -DTCSC_FUSED_PF_LAST=1
+FDEF_nop := -DTCSC_UNIT_NOP='"4"'
+FDEF_w0 := -DTCSC_PRODUCE_WAIT0
+FDEF_dl := -DTCSC_PRODUCE_DELAY
+FDEF_nl := -DTCSC_FUSED_DIAG_NOLOOP=1
+FDEF_pu := -DTCSC_FUSED_DIAG_PURE=1
+FDEF_st := -DTCSC_FUSED_STAMPS=1
+lib/abl/libtcsc_amd_f%.so: $(SRC)/tcsc_kernels.hip $(SRC)/tcsc_api.cpp $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o $(HDRS) $(SRC)/gather_asm.inc
+	@mkdir -p lib/abl $(OBJ)/abl
+	$(HIPCC) $(HIPFLAGS) $(FDEF_$*) -c $(SRC)/tcsc_kernels.hip -o $(OBJ)/abl/k_f$*.o
+	$(HIPCC) $(HIPFLAGS) $(FDEF_$*) -c $(SRC)/tcsc_api.cpp -o $(OBJ)/abl/a_f$*.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)/abl/k_f$*.o $(OBJ)/abl/a_f$*.o $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o -lpthread -L$(ROCM)/lib -lrocblas -Wl,-rpath,$(ROCM)/lib
