@@ -333,6 +333,13 @@ hipError_t launch_small_m(const float* X, int M, int K, const int* cp, const int
 // X (M x K) -> x3 (M x ldk bf16, [h | m | l | 0..]); flags[m] = 1 for the
 // rows the fixup recomputes, 0 otherwise (every row, every call).
 hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int* flags, hipStream_t st);
+// the fused-split path (k_gemm3x + k_fixup_x): X read directly, no X3
+bool mfma_fused_ok(const float* X, int K);
+hipError_t mfma_gemm3x(const float* X, const uint16_t* w3, int ldk, int M, int N, int K, const float* B, float* Y,
+                       int ldy, bool prelu, float a, int* flags, hipStream_t st);
+hipError_t mfma_fixup_x(const float* X, int M, int K, const int* cp, const int* cn, const int* crp, const int* crn,
+                        int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
+                        const int* flags, hipStream_t st);
 // k_gemm3: Y = act(x3 . w3^T + B) on the matrix cores (bias after the sum).
 hipError_t mfma_gemm3(const uint16_t* x3, const uint16_t* w3, int ldk, int M, int N, const float* B, float* Y,
                       int ldy, bool prelu, float a, hipStream_t st);
