@@ -911,14 +911,23 @@ __device__ __forceinline__ void store4_sc1(char* base, unsigned o, unsigned st, 
 // (ds_read_b128 x 4, the 4 x 4 block of lane l transposed in registers,
 // 4 x global_store_dwordx4 sc1: write-through, so no L2 write-back is needed
 // before the piece is signalled).
-__device__ __forceinline__ void unit_store(const char* lds_slot, float* XT, int ldxt, int m0, int k0, int lane) {
+struct UnitRegs {
+    f32x4v x0, x1, x2, x3;
+};
+__device__ __forceinline__ UnitRegs unit_load(const char* lds_slot, int lane) {
     const f32x4v* s = reinterpret_cast<const f32x4v*>(lds_slot) + lane;
-    const f32x4v x0 = s[0], x1 = s[64], x2 = s[128], x3 = s[192];
+    return UnitRegs{s[0], s[64], s[128], s[192]};
+}
+__device__ __forceinline__ void unit_store_regs(const UnitRegs& u, float* XT, int ldxt, int m0, int k0, int lane) {
+    const f32x4v x0 = u.x0, x1 = u.x1, x2 = u.x2, x3 = u.x3;
     char* base = reinterpret_cast<char*>(XT + (size_t)k0 * ldxt + m0);
     const unsigned o = 16u * lane, st = (unsigned)ldxt * 4u;
     const f32x4v r0 = {x0.x, x1.x, x2.x, x3.x}, r1 = {x0.y, x1.y, x2.y, x3.y};
     const f32x4v r2 = {x0.z, x1.z, x2.z, x3.z}, r3 = {x0.w, x1.w, x2.w, x3.w};
     store4_sc1(base, o, st, r0, r1, r2, r3);
+}
+__device__ __forceinline__ void unit_store(const char* lds_slot, float* XT, int ldxt, int m0, int k0, int lane) {
+    unit_store_regs(unit_load(lds_slot, lane), XT, ldxt, m0, k0, lane);
 }
 
 // The same unit through registers (the timeout path: one wave, no LDS).
@@ -1005,14 +1014,26 @@ __device__ __forceinline__ ItemRec load_rec(const char* lds) {
 // next chunk at which a stage can move (the caller skips the step until
 // then: no LDS read per chunk), INT_MAX once the wave has nothing left.
 __device__ __forceinline__ int produce_step(char* lds, int wave, int lane, int t, bool drain) {
+    // Everything but the stream prefetch issued at the end of the last chunk
+    // (issued after every unit DMA and store of this wave): the DMA / stores
+    // a due stage waits for are >= 1 chunk old (steps are >= 1 chunk apart),
+    // so this costs ~nothing.  Then every LDS read of the step at once (one
+    // round trip through the LDS queue, which the gather keeps full): state,
+    // record, the slot's unit.
+    if (drain)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPfS ? 1 : 0) : "memory");
     int4* stp = reinterpret_cast<int4*>(lds + kFusedStateOff + 64) + (wave - kProdWave0);
+    const char* slot_ptr = lds + kFusedSlotOff + (wave - kProdWave0) * kUnitBytes;
     const int4 st = *stp;
+    const ItemRec r = load_rec(lds);
+    const UnitRegs ur = unit_load(slot_ptr, lane);
     int u_next = __builtin_amdgcn_readfirstlane(st.x), d_u = __builtin_amdgcn_readfirstlane(st.y),
         s_u = __builtin_amdgcn_readfirstlane(st.z);
     const int tw = __builtin_amdgcn_readfirstlane(st.w);
     if (u_next == 0x7fffffff && d_u < 0 && s_u < 0) return 0x7fffffff;
     int tD = tw & 0xffff, tS = (tw >> 16) & 0xffff;
-    const ItemRec r = load_rec(lds);
     const bool sig_now = s_u >= 0 && (drain || t >= tS + kSigDelay);
     const bool store_now = d_u >= 0 && (s_u < 0 || sig_now) && (drain || t >= tD + kStoreDelay);
     const bool dma_now = (d_u < 0 || store_now) && u_next < r.U &&
@@ -1026,23 +1047,15 @@ __device__ __forceinline__ int produce_step(char* lds, int wave, int lane, int t
         return max(tn, t + 1);
     };
     if (!sig_now && !store_now && !dma_now) return next_t();
-    // everything but the stream prefetch issued at the end of the last chunk
-    // (issued after every unit DMA and store of this wave): the DMA/stores
-    // waited for are >= kStoreDelay-1 chunks old and have landed
-    if (drain)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (sig_now || store_now)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPfS ? 1 : 0) : "memory");
     if (sig_now) {
         const int p = s_u / r.upc;
         unsigned* crow = reinterpret_cast<unsigned*>(r.crow);
         if (s_u + r.An >= min(r.U, (p + 1) * r.upc) && lane == 0) piece_signal(crow + ((size_t)p << (r.pcs + 1)));
         s_u = -1;
     }
-    const char* slot_ptr = lds + kFusedSlotOff + (wave - kProdWave0) * kUnitBytes;
     if (store_now) {
         float* XT = reinterpret_cast<float*>(r.xtrow);
-        unit_store(slot_ptr, XT + (size_t)(r.k_lo + kUnitK * d_u) * r.ldxt, r.ldxt, 0, 0, lane);
+        unit_store_regs(ur, XT + (size_t)(r.k_lo + kUnitK * d_u) * r.ldxt, r.ldxt, 0, 0, lane);
         s_u = d_u;
         tS = t;
         d_u = -1;
@@ -1086,6 +1099,37 @@ __device__ __forceinline__ void wait_piece(const char* lds, int p, int lane, boo
         }
         __builtin_amdgcn_s_sleep(2);
     }
+}
+
+// Poll wave, right after a chunk barrier (the LDS queue is short then):
+// whether piece pc_next (checked before the next barrier; -1: none) is
+// complete by its probe, and the probe of piece pp (-1: none) for the check
+// kProbeAhead chunks later.  One LDS round trip for the record and the word.
+__device__ __forceinline__ bool poll_after_barrier(const char* lds, int pc_next, bool probed, int pp, int pcs,
+                                                   int lane) {
+    const int4* rec = reinterpret_cast<const int4*>(lds + kFusedStateOff);
+    if (pc_next >= 0 && probed)  // the probe is >= kProbeAhead - 1 chunks old: all but the last stream prefetch
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPfS ? 1 : 0) : "memory");
+    const int4 c2 = rec[2], c3 = rec[3];
+    const unsigned v = reinterpret_cast<const volatile unsigned*>(lds + kFusedProbeOff)[(pc_next < 0 ? 0 : pc_next) & 7];
+    bool ready = true;
+    if (pc_next >= 0) {
+        ready = false;
+        if (probed) {
+            const int U = __builtin_amdgcn_readfirstlane(c2.x), upc = __builtin_amdgcn_readfirstlane(c2.y),
+                      An = __builtin_amdgcn_readfirstlane(c2.z);
+            const unsigned tgt = (unsigned)min(An, min(U, (pc_next + 1) * upc) - pc_next * upc);
+            ready = (unsigned)__builtin_amdgcn_readfirstlane((int)v) >= tgt;
+        }
+    }
+    if (pp >= 0) {
+        const unsigned long long cr = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(c3.w) << 32) |
+                                      (unsigned)__builtin_amdgcn_readfirstlane(c3.z);
+        const unsigned* c = reinterpret_cast<const unsigned*>(cr) + ((size_t)pp << (pcs + 1));
+        if (lane == 0)
+            piece_probe((unsigned)reinterpret_cast<uintptr_t>(lds) + kFusedProbeOff + 4u * (unsigned)(pp & 7), c);
+    }
+    return ready;
 }
 
 // Poll wave, kProbeAhead chunks before the check of piece p: the probe of
@@ -1297,13 +1341,17 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
                 // for the poll wave, the next chunk a producer wave can act at
                 const int pcs = opaque_s(__builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(lds + kFusedStateOff)[12]));
                 int t_evt = 0;
+                bool ready = false;  // poll wave: the next check's piece was seen complete after the last barrier
+                const int nloc = c_end - c_begin, pmask = (1 << pcs) - 1;
                 for (int c = c_begin; c < c_end; ++c) {
-                    if (!TCSC_FUSED_DIAG_NOLOOP && wave == kPollWave) {  // chunk c+kNBuf-1 is DMA'd right after this barrier
-                        const int t2 = c + kNBuf - 1 - c_begin;
-                        if (t2 < c_end - c_begin && (t2 & ((1 << pcs) - 1)) == 0) {
+                    const int t = c - c_begin;
+                    if (!TCSC_FUSED_DIAG_NOLOOP && wave == kPollWave) {  // chunk t+kNBuf-1 is DMA'd right after this barrier
+                        const int t2 = t + kNBuf - 1;
+                        if (t2 < nloc && (t2 & pmask) == 0 && !ready) {
                             const unsigned long long w0 = FST_NOW();
-                            wait_piece(lds, t2 >> pcs, lane, t2 >= kNBuf - 1 + kProbeAhead);
+                            wait_piece(lds, t2 >> pcs, lane, false);
                             FST_ADD(lds, 4, FST_NOW() - w0);
+                            FST_ADD(lds, 5, 1);
                         }
                     }
 #if TCSC_FUSED_STAMPS
@@ -1315,18 +1363,25 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
                     if (wave == 0) FST_ADD(lds, 6, FST_NOW() - b0);
 #endif
                     if (dma_wave) dma_next_chunk(dma, dbuf);
-                    gather_stream(sb, sbt, cur, lane, mask, acc);
-                    load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
-                    if (!TCSC_FUSED_DIAG_NOLOOP && prod_wave && c - c_begin >= t_evt) {
+                    // producer and poll work right after the barrier, while the LDS queue is short
+                    if (!TCSC_FUSED_DIAG_NOLOOP && prod_wave && t >= t_evt) {
                         const unsigned long long p0 = FST_NOW();
-                        t_evt = produce_step(lds, wave, opaque_v(lane), c - c_begin, false);
+                        t_evt = produce_step(lds, wave, opaque_v(lane), t, false);
                         FST_ADD(lds, 3, FST_NOW() - p0);
                         FST_ADD(lds, 7, 1);
                     }
-                    if (!TCSC_FUSED_DIAG_NOLOOP && wave == kPollWave) {  // probe the counter this wave checks kProbeAhead chunks from now
-                        const int t3 = c + kNBuf - 1 + kProbeAhead - c_begin;
-                        if (t3 < c_end - c_begin && (t3 & ((1 << pcs) - 1)) == 0) probe_issue(lds, t3 >> pcs, pcs, opaque_v(lane));
+                    if (!TCSC_FUSED_DIAG_NOLOOP && wave == kPollWave) {
+                        const int tn = t + kNBuf;                 // the check before the next barrier
+                        const int tp = t + kNBuf - 1 + kProbeAhead;  // the probe for the check kProbeAhead chunks on
+                        const bool chk = tn < nloc && (tn & pmask) == 0;
+                        const bool prb = tp < nloc && (tp & pmask) == 0;
+                        ready = true;
+                        if (chk || prb)
+                            ready = poll_after_barrier(lds, chk ? tn >> pcs : -1, tn >= kNBuf - 1 + kProbeAhead,
+                                                       prb ? tp >> pcs : -1, pcs, opaque_v(lane));
                     }
+                    gather_stream(sb, sbt, cur, lane, mask, acc);
+                    load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
                     pf_issue(cur);
                     dbuf = dbuf == kNBuf - 1 ? 0 : dbuf + 1;
                 }

@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "sparse-matrix-multiplication-benchmark_am
 import tcsc_amd  # noqa: E402
 import torch  # noqa: E402
 
-SLOTS = ["prologue", "chunk loop", "epilogue", "producer steps", "poll checks", "-", "wave0 barrier waits",
+SLOTS = ["prologue", "chunk loop", "epilogue", "producer steps", "blocking polls", "blocking poll count", "wave0 barrier waits",
          "producer step count"]
 
 
@@ -68,7 +68,7 @@ def main(M=4096, K=16384, N=16384, density=0.02, reps=5):
         col = a[:, i]
         frac = col.mean() / tot.mean()
         print(f"  {name:22s} mean {col.mean():12.0f}  max {col.max():12.0f}  ({100 * frac:5.1f} % of item time)"
-              if i != 7 else f"  {name:22s} mean {col.mean():12.1f}")
+              if i not in (5, 7) else f"  {name:22s} mean {col.mean():12.1f}")
     plan.destroy()
 
 
