@@ -820,7 +820,7 @@ constexpr int kPollLimit = 1 << 12;
 #define TCSC_FUSED_STAMPS 0
 #endif
 #if TCSC_FUSED_STAMPS
-__device__ unsigned long long g_fstamp[4096 * 8];
+__device__ unsigned long long g_fstamp[4096 * 16];
 #define FST_NOW() ((unsigned long long)__builtin_amdgcn_s_memtime())
 #define FST_ADD(lds, slot, v)                                                                        \
     do {                                                                                             \
@@ -838,6 +838,53 @@ __device__ unsigned long long g_fstamp[4096 * 8];
 __device__ __forceinline__ int xcd_slot(int b, int P) {
     const int q = P >> 3, r = P & 7, x = b & 7;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+// Item schedule (TCSC_FUSED_XCD_RANGES, default): XCD x (the workgroups
+// b = x mod 8, MI355X_MICROARCH.md "Workgroup dispatch") takes a contiguous
+// range of the group-major item order, its Wx workgroups item base + j,
+// base + j + Wx, ...: a group's column blocks (one row tile of X^T) stay on
+// one XCD's L2 across rounds, as k_stream's tile order keeps them.  The
+// other schedule deals item slot + r*P (a group's items in one round, but
+// split over two XCDs, each reading the row tile into its own L2).
+#ifndef TCSC_FUSED_PROD_LATE  // A/B: producer steps after the gather instead of after the barrier
+#define TCSC_FUSED_PROD_LATE 0
+#endif
+#ifndef TCSC_FUSED_PROD_PRIO  // A/B: producer steps at raised wave priority
+#define TCSC_FUSED_PROD_PRIO 0
+#endif
+#ifndef TCSC_FUSED_XCD_RANGES
+#define TCSC_FUSED_XCD_RANGES 1
+#endif
+struct XcdRange {
+    int base, end, W;  // the XCD's items [base, end), its workgroups
+};
+__device__ __forceinline__ XcdRange xcd_range(int x, int P, int n_items) {
+    const int q = P >> 3, rr = P & 7;
+    const int W = q + (x < rr ? 1 : 0), pre = x * q + min(x, rr);
+    return XcdRange{(int)((long long)n_items * pre / P), (int)((long long)n_items * (pre + W) / P), W};
+}
+__device__ __forceinline__ int first_item(int b, int P, int n_items) {
+    if (!TCSC_FUSED_XCD_RANGES) return xcd_slot(b, P);
+    const XcdRange g = xcd_range(b & 7, P, n_items);
+    const int i = g.base + (b >> 3);
+    return i < g.end ? i : n_items;
+}
+__device__ __forceinline__ int next_item(int item, int b, int P, int n_items) {
+    if (!TCSC_FUSED_XCD_RANGES) return item + P;
+    const XcdRange g = xcd_range(b & 7, P, n_items);
+    const int i = item + g.W;
+    return i < g.end ? i : n_items;
+}
+// The end of the members of the group starting at gi0: the group's items that
+// run in the same round as gi0 (same XCD range and round, or round-robin round).
+__device__ __forceinline__ int members_end(int gi0, int ncb, int P, int n_items) {
+    if (!TCSC_FUSED_XCD_RANGES) return min(gi0 + ncb, (gi0 / P + 1) * P);
+    int x = 0;
+    XcdRange g = xcd_range(0, P, n_items);
+    while (x < 7 && gi0 >= g.end) g = xcd_range(++x, P, n_items);
+    const int round_end = g.base + ((gi0 - g.base) / g.W + 1) * g.W;
+    return min(min(gi0 + ncb, g.end), round_end);
 }
 
 // Piece counters: 32-bit, two sets used by alternate launches (epoch
@@ -998,8 +1045,8 @@ __device__ __forceinline__ ItemRec load_rec(const char* lds) {
 
 // One production step of a producer wave, at chunk t of the item (relative
 // to its first chunk).  An agent's units move through three stages, one unit
-// per stage at a time (producer state in LDS: next unit, the unit in the LDS
-// slot and when its DMA was issued, the unit stored and when):
+// per stage at a time (ProdState, in registers: next unit, the unit in the
+// LDS slot and when its DMA was issued, the unit stored and when):
 //   DMA: unit u of piece p is issued once t >= (p - lead) * pc, i.e. about
 //        lead pieces ahead of the chunk that polls p -- production keeps a
 //        fixed distance ahead of the gather instead of racing it (racing
@@ -1013,64 +1060,69 @@ __device__ __forceinline__ ItemRec load_rec(const char* lds) {
 // `drain` (after the chunk loop) moves every stage at once.  Returns the
 // next chunk at which a stage can move (the caller skips the step until
 // then: no LDS read per chunk), INT_MAX once the wave has nothing left.
-__device__ __forceinline__ int produce_step(char* lds, int wave, int lane, int t, bool drain) {
-    // Everything but the stream prefetch issued at the end of the last chunk
-    // (issued after every unit DMA and store of this wave): the DMA / stores
-    // a due stage waits for are >= 1 chunk old (steps are >= 1 chunk apart),
-    // so this costs ~nothing.  Then every LDS read of the step at once (one
-    // round trip through the LDS queue, which the gather keeps full): state,
-    // record, the slot's unit.
-    if (drain)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPfS ? 1 : 0) : "memory");
-    int4* stp = reinterpret_cast<int4*>(lds + kFusedStateOff + 64) + (wave - kProdWave0);
+struct ProdState {
+    int u_next, d_u, s_u, tD, tS;  // next unit (INT_MAX: none), unit in the slot, unit stored (-1: none)
+};
+
+__device__ __forceinline__ int prod_next_t(const ProdState& ps, int U, int upc, int lead, int pcs, int t) {
+    int tn = 0x7fffffff;
+    if (ps.s_u >= 0) tn = min(tn, ps.tS + kSigDelay);
+    if (ps.d_u >= 0) tn = min(tn, ps.tD + kStoreDelay);
+    else if (ps.u_next < U) tn = min(tn, (ps.u_next / upc - lead) << pcs);
+    return max(tn, t + 1);
+}
+
+__device__ __forceinline__ int produce_step(char* lds, int wave, int lane, int t, bool drain, ProdState& ps,
+                                            const ItemRec& r) {
+    if (ps.u_next == 0x7fffffff && ps.d_u < 0 && ps.s_u < 0) return 0x7fffffff;
     const char* slot_ptr = lds + kFusedSlotOff + (wave - kProdWave0) * kUnitBytes;
-    const int4 st = *stp;
-    const ItemRec r = load_rec(lds);
-    const UnitRegs ur = unit_load(slot_ptr, lane);
-    int u_next = __builtin_amdgcn_readfirstlane(st.x), d_u = __builtin_amdgcn_readfirstlane(st.y),
-        s_u = __builtin_amdgcn_readfirstlane(st.z);
-    const int tw = __builtin_amdgcn_readfirstlane(st.w);
-    if (u_next == 0x7fffffff && d_u < 0 && s_u < 0) return 0x7fffffff;
-    int tD = tw & 0xffff, tS = (tw >> 16) & 0xffff;
-    const bool sig_now = s_u >= 0 && (drain || t >= tS + kSigDelay);
-    const bool store_now = d_u >= 0 && (s_u < 0 || sig_now) && (drain || t >= tD + kStoreDelay);
-    const bool dma_now = (d_u < 0 || store_now) && u_next < r.U &&
-                         (drain || t >= ((u_next / r.upc - r.lead) << r.pcs));
-    // the next chunk at which a stage can move
-    auto next_t = [&]() {
-        int tn = 0x7fffffff;
-        if (s_u >= 0) tn = min(tn, tS + kSigDelay);
-        if (d_u >= 0) tn = min(tn, tD + kStoreDelay);
-        else if (u_next < r.U) tn = min(tn, (u_next / r.upc - r.lead) << r.pcs);
-        return max(tn, t + 1);
-    };
-    if (!sig_now && !store_now && !dma_now) return next_t();
+    const unsigned long long q1 = FST_NOW();
+    const bool sig_now = ps.s_u >= 0 && (drain || t >= ps.tS + kSigDelay);
+    const bool store_now = ps.d_u >= 0 && (ps.s_u < 0 || sig_now) && (drain || t >= ps.tD + kStoreDelay);
+    const bool dma_now = (ps.d_u < 0 || store_now) && ps.u_next < r.U &&
+                         (drain || t >= ((ps.u_next / r.upc - r.lead) << r.pcs));
+    if (!sig_now && !store_now && !dma_now) return prod_next_t(ps, r.U, r.upc, r.lead, r.pcs, t);
+    // A signal needs this wave's stores complete: vmcnt(0) (the guide's
+    // hand-off rule); they are >= kSigDelay chunks old, so it waits at most
+    // for the last chunk's stream prefetch.  A store needs the slot's LDS-DMA
+    // landed: it is older than the >= kStoreDelay stream prefetches issued
+    // since (one per chunk), and loads return in order, so vmcnt(kStoreDelay)
+    // is enough and the recent prefetches stay in flight.
+    if (drain || sig_now)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (store_now)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPfS ? kStoreDelay : 0) : "memory");
+    const unsigned long long q2 = FST_NOW();
+    FST_ADD(lds, 9, q2 - q1);
     if (sig_now) {
-        const int p = s_u / r.upc;
+        const int p = ps.s_u / r.upc;
         unsigned* crow = reinterpret_cast<unsigned*>(r.crow);
-        if (s_u + r.An >= min(r.U, (p + 1) * r.upc) && lane == 0) piece_signal(crow + ((size_t)p << (r.pcs + 1)));
-        s_u = -1;
+        if (ps.s_u + r.An >= min(r.U, (p + 1) * r.upc) && lane == 0)
+            piece_signal(crow + ((size_t)p << (r.pcs + 1)));
+        ps.s_u = -1;
     }
+    const unsigned long long q3 = FST_NOW();
+    FST_ADD(lds, 12, q3 - q2);
     if (store_now) {
         float* XT = reinterpret_cast<float*>(r.xtrow);
-        unit_store_regs(ur, XT + (size_t)(r.k_lo + kUnitK * d_u) * r.ldxt, r.ldxt, 0, 0, lane);
-        s_u = d_u;
-        tS = t;
-        d_u = -1;
+        unit_store(slot_ptr, XT + (size_t)(r.k_lo + kUnitK * ps.d_u) * r.ldxt, r.ldxt, 0, 0, lane);
+        ps.s_u = ps.d_u;
+        ps.tS = t;
+        ps.d_u = -1;
     }
+    const unsigned long long q4 = FST_NOW();
+    FST_ADD(lds, 10, q4 - q3);
     if (dma_now) {
         const float* X = reinterpret_cast<const float*>(r.xrow);
-        unit_dma(X + r.k_lo + kUnitK * u_next, r.K, r.mmax + 1, 0, 0,
+        unit_dma(X + r.k_lo + kUnitK * ps.u_next, r.K, r.mmax + 1, 0, 0,
                  (unsigned)reinterpret_cast<uintptr_t>(slot_ptr), lane);
-        d_u = u_next;
-        tD = t;
-        u_next = u_next + r.An < r.U ? u_next + r.An : 0x7fffffff;
+        ps.d_u = ps.u_next;
+        ps.tD = t;
+        ps.u_next = ps.u_next + r.An < r.U ? ps.u_next + r.An : 0x7fffffff;
     }
-    if (lane == 0) *stp = make_int4(u_next, d_u, s_u, (tS << 16) | tD);
-    if (u_next == 0x7fffffff && d_u < 0 && s_u < 0) return 0x7fffffff;
-    return next_t();
+    FST_ADD(lds, 11, FST_NOW() - q4);
+    if (ps.u_next == 0x7fffffff && ps.d_u < 0 && ps.s_u < 0) return 0x7fffffff;
+    return prod_next_t(ps, r.U, r.upc, r.lead, r.pcs, t);
 }
 
 // Wave 6 before the barrier ahead of chunk c+kNBuf-1's DMA: when that chunk
@@ -1175,10 +1227,10 @@ __device__ __forceinline__ ItemPos item_pos(int item) {
 
 template <bool BIAS_FIRST, bool PRELU, int OUT>
 __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const FusedArgs A) {
-    __shared__ __attribute__((aligned(16))) char lds[kFusedLdsBytes + (TCSC_FUSED_STAMPS ? 64 : 0)];
+    __shared__ __attribute__((aligned(16))) char lds[kFusedLdsBytes + (TCSC_FUSED_STAMPS ? 128 : 0)];
     (void)A;  // every field is read through fargs()
 #if TCSC_FUSED_STAMPS
-    if (threadIdx.x < 8) reinterpret_cast<unsigned long long*>(lds + kFusedLdsBytes0)[threadIdx.x] = 0;
+    if (threadIdx.x < 16) reinterpret_cast<unsigned long long*>(lds + kFusedLdsBytes0)[threadIdx.x] = 0;
     __syncthreads();
 #endif
     {
@@ -1195,7 +1247,8 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
             cnt[2 * (size_t)i] = 0u;
     }
 
-    for (int item = xcd_slot(blockIdx.x, gridDim.x); item < fargs()->n_items; item = opaque_s(item + (int)gridDim.x)) {
+    for (int item = first_item(blockIdx.x, gridDim.x, fargs()->n_items); item < fargs()->n_items;
+         item = opaque_s(next_item(item, blockIdx.x, gridDim.x, fargs()->n_items))) {
         // ---- item prologue: this agent's units of the first `lead` pieces, the record, piece 0 ----
         const unsigned long long fst0 = FST_NOW();
         {
@@ -1208,7 +1261,7 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
             const int ncb = F->ncb, nch = F->nch, K = F->K, M = F->M;
             // the group's members: its items in the group's first round
             const int gi0 = q.grp * ncb;
-            const int mem_end = min(gi0 + ncb, (gi0 / P + 1) * P);
+            const int mem_end = members_end(gi0, ncb, P, F->n_items);
             const int An = kProdWaves * (mem_end - gi0);
             const int k_lo = q.c_begin * kTK;
             const int U = q.c_begin < q.c_end ? (min(q.c_end * kTK, K) - k_lo + kUnitK - 1) / kUnitK : 0;
@@ -1341,6 +1394,14 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
                 // for the poll wave, the next chunk a producer wave can act at
                 const int pcs = opaque_s(__builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(lds + kFusedStateOff)[12]));
                 int t_evt = 0;
+                ProdState ps{0x7fffffff, -1, -1, 0, 0};
+                // the item record in registers for the loop (a producer step or a
+                // poll then reads no LDS for it: the gather keeps the LDS queue long)
+                const ItemRec rec = load_rec(lds);
+                if (prod_wave) {  // the item prologue's hand-over: the agent's next unit
+                    const int4 st = reinterpret_cast<const int4*>(lds + kFusedStateOff + 64)[wave - kProdWave0];
+                    ps.u_next = __builtin_amdgcn_readfirstlane(st.x);
+                }
                 bool ready = false;  // poll wave: the next check's piece was seen complete after the last barrier
                 const int nloc = c_end - c_begin, pmask = (1 << pcs) - 1;
                 for (int c = c_begin; c < c_end; ++c) {
@@ -1364,9 +1425,11 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
 #endif
                     if (dma_wave) dma_next_chunk(dma, dbuf);
                     // producer and poll work right after the barrier, while the LDS queue is short
-                    if (!TCSC_FUSED_DIAG_NOLOOP && prod_wave && t >= t_evt) {
+                    if (!TCSC_FUSED_DIAG_NOLOOP && !TCSC_FUSED_PROD_LATE && prod_wave && t >= t_evt) {
                         const unsigned long long p0 = FST_NOW();
-                        t_evt = produce_step(lds, wave, opaque_v(lane), t, false);
+                        if (TCSC_FUSED_PROD_PRIO) __builtin_amdgcn_s_setprio(3);
+                        t_evt = produce_step(lds, wave, opaque_v(lane), t, false, ps, rec);
+                        if (TCSC_FUSED_PROD_PRIO) __builtin_amdgcn_s_setprio(0);
                         FST_ADD(lds, 3, FST_NOW() - p0);
                         FST_ADD(lds, 7, 1);
                     }
@@ -1382,12 +1445,17 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
                     }
                     gather_stream(sb, sbt, cur, lane, mask, acc);
                     load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
+                    if (!TCSC_FUSED_DIAG_NOLOOP && TCSC_FUSED_PROD_LATE && prod_wave && t >= t_evt) {
+                        if (TCSC_FUSED_PROD_PRIO) __builtin_amdgcn_s_setprio(3);
+                        t_evt = produce_step(lds, wave, opaque_v(lane), t, false, ps, rec);
+                        if (TCSC_FUSED_PROD_PRIO) __builtin_amdgcn_s_setprio(0);
+                    }
                     pf_issue(cur);
                     dbuf = dbuf == kNBuf - 1 ? 0 : dbuf + 1;
                 }
                 // units still in flight (a group whose gather ends first)
                 if (prod_wave)
-                    while (produce_step(lds, wave, opaque_v(lane), 0xffff, true) != 0x7fffffff) {
+                    while (produce_step(lds, wave, opaque_v(lane), 0xffff, true, ps, rec) != 0x7fffffff) {
                     }
                 asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             }
@@ -1497,8 +1565,8 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
     // the last workgroup to finish advances the epoch (the counter wraps to 0)
     __syncthreads();
 #if TCSC_FUSED_STAMPS
-    if (threadIdx.x < 8)
-        atomicAdd(&g_fstamp[(blockIdx.x & 4095) * 8 + threadIdx.x],
+    if (threadIdx.x < 16)
+        atomicAdd(&g_fstamp[(blockIdx.x & 4095) * 16 + threadIdx.x],
                   reinterpret_cast<const unsigned long long*>(lds + kFusedLdsBytes0)[threadIdx.x]);
 #endif
     if (threadIdx.x == 0) {
@@ -1949,7 +2017,7 @@ static hipError_t launch_fused_t(const GemmArgs& g, int slices, hipStream_t st) 
 }  // namespace tcsc
 extern "C" int tcsc_diag_fused_stamps(unsigned long long* out, int n) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tcsc::g_fstamp), (size_t)n * 8) != hipSuccess) return -1;
-    static unsigned long long zero[4096 * 8];
+    static unsigned long long zero[4096 * 16];
     return hipMemcpyToSymbol(HIP_SYMBOL(tcsc::g_fstamp), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 namespace tcsc {

@@ -30,6 +30,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "tcsc_internal.h"
 
@@ -367,9 +368,12 @@ __device__ inline void split_pair(float x0, float x1, uint32_t& h, uint32_t& m, 
     l = (f2u(s1) & 0xffff0000u) | (f2u(s0) >> 16);
 }
 
-__device__ inline bool needs_fixup(float x) {
-    const uint32_t u = f2u(x);
-    return (u & 0x7f800000u) == 0x7f800000u || (x != 0.0f && fabsf(x) < 0x1p-100f);
+// Branch-free row-flag test (bit 31 set when x needs the fixup): with
+// a = |x| bits, non-finite <=> a + 2^23 >= 2^31, tiny nonzero <=>
+// 0 < a < bits(2^-100) = 27 << 23 (a - (27 << 23) negative and -a negative).
+__device__ inline uint32_t fixup_bit31(float x) {
+    const uint32_t a = f2u(x) & 0x7fffffffu;
+    return (a + 0x00800000u) | ((a - (27u << 23)) & (0u - a));
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -442,6 +446,10 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3x(const float* __restrict
     dma(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    // the k loop, compiled twice: with the row-flag test (column-tile-0 waves
+    // of column 0) and without (everyone else: no extra VALU in the loop)
+    auto kloop = [&](auto flags_c) {
+    constexpr bool FLAGS = decltype(flags_c)::value;
     for (int t = 0; t < ksteps; ++t) {
         const int buf = t & 1;
         if (t + 1 < ksteps) dma(t + 1, buf ^ 1);
@@ -454,12 +462,10 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3x(const float* __restrict
             const char* ab = sb + (wr * FI + i) * 2048;
             const f32x4 x0 = *reinterpret_cast<const f32x4*>(ab + aoff[0]);
             const f32x4 x1 = *reinterpret_cast<const f32x4*>(ab + aoff[1]);
-            if (do_flags) {
-                const uint32_t bad = (uint32_t)needs_fixup(x0.x) | (uint32_t)needs_fixup(x0.y) |
-                                     (uint32_t)needs_fixup(x0.z) | (uint32_t)needs_fixup(x0.w) |
-                                     (uint32_t)needs_fixup(x1.x) | (uint32_t)needs_fixup(x1.y) |
-                                     (uint32_t)needs_fixup(x1.z) | (uint32_t)needs_fixup(x1.w);
-                fl |= bad << i;
+            if constexpr (FLAGS) {
+                const uint32_t bad = fixup_bit31(x0.x) | fixup_bit31(x0.y) | fixup_bit31(x0.z) | fixup_bit31(x0.w) |
+                                     fixup_bit31(x1.x) | fixup_bit31(x1.y) | fixup_bit31(x1.z) | fixup_bit31(x1.w);
+                fl |= (bad >> 31) << i;
             }
             uint32_t h0, h1, h2, h3, mm0, mm1, mm2, mm3, l0, l1, l2, l3;
             split_pair(x0.x, x0.y, h0, mm0, l0);
@@ -469,16 +475,23 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3x(const float* __restrict
             const u32x4 hv = {h0, h1, h2, h3}, mv = {mm0, mm1, mm2, mm3}, lv = {l0, l1, l2, l3};
             const bf16x8 ah = __builtin_bit_cast(bf16x8, hv), am = __builtin_bit_cast(bf16x8, mv),
                          al = __builtin_bit_cast(bf16x8, lv);
+            // part-major over j: an accumulator's next MFMA is FJ MFMAs away
+            // (back-to-back MFMAs on one accumulator stall on its latency)
 #pragma unroll
-            for (int j = 0; j < FJ; ++j) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bfr[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bfr[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bfr[j], acc[i][j], 0, 0, 0);
-            }
+            for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bfr[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bfr[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bfr[j], acc[i][j], 0, 0, 0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
+    };
+    if (do_flags)
+        kloop(std::true_type{});
+    else
+        kloop(std::false_type{});
 
     if (do_flags) {  // lanes l, l^16, l^32, l^48 hold row l & 15 of each block
         fl |= (uint32_t)__shfl_xor((int)fl, 16);

@@ -1,18 +1,23 @@
 """The reference's own harness, unmodified, on the GPU (the north star's
 "drops in under the existing main.cpp").
 
-oracle/_ref/main_amd is /root/reference/main.cpp compiled in place against
-its own headers, together with the reference's own dense/dense.c, and linked
-against libtcsc_amd.so in place of sparse/tcsc.c (oracle/Makefile target
-`harness`; the g++-mangled names come from csrc/tcsc_cxx_abi.cpp).  The
-executable defines gemm_basic, compare and init_rand_* itself (its
-definitions take precedence over the library's), so the harness validates
-the GPU with the reference's own oracle and data generators: only the
-tcsc_* calls reach the library (test_main_amd_links_reference_dense checks
-this with nm).  For each of its five cases (main.cpp:258-264) it validates
-every tcsc_sgemm_* variant with its own compare() (abs tol 1e-4,
-dense.c:42-59) against its own CPU gemm_basic and exit(1)s on a mismatch
-(main.cpp:299-368), then times all six functions with its cycle counter.
+oracle/_ref/main_amd_rv is /root/reference/main.cpp compiled in place
+against its own headers, together with the reference's own dense/dense.c,
+and linked against libtcsc_amd.so in place of sparse/tcsc.c (oracle/Makefile
+target `harness`; the g++-mangled names come from csrc/tcsc_cxx_abi.cpp).
+The executable defines gemm_basic, compare and init_rand_* itself, so the
+harness validates the GPU with the reference's own oracle, compare() and
+data generators (test_main_amd_links_reference_dense checks this with nm).
+One link-level change (oracle/harness_wrap.cpp, --wrap): the >= 1,020
+TIMING calls per case of main.cpp's dense gemm_basic go to the library's
+bit-identical restatement, because dense.c's naive loop would make the run
+take hours; the one VALIDATION call per case (main.cpp:306, the refY that
+compare() checks against) is the reference's, and the test requires the
+wrapper's exit report to say so (5 calls).  For each of its five cases
+(main.cpp:258-264) it validates every tcsc_sgemm_* variant with its own
+compare() (abs tol 1e-4, dense.c:42-59) against that refY and exit(1)s on a
+mismatch (main.cpp:299-368), then times all six functions with its cycle
+counter.
 
 The test runs it to the end as a child process and requires "[OK] All
 validation tests passed!" for all five cases, no "[ERROR]" line, exit status
@@ -37,14 +42,14 @@ from conftest import PKG, ROOT
 
 pytestmark = [pytest.mark.gpu, pytest.mark.config_parity]
 
-BIN = os.path.join(ROOT, "oracle", "_ref", "main_amd")
+BIN = os.path.join(ROOT, "oracle", "_ref", "main_amd_rv")
 CASES = [(1, 512, 2048), (1, 1024, 4096), (1, 2048, 8192), (256, 512, 2048), (256, 1024, 4096)]
 OK = "[OK] All validation tests passed!"
 
 
 @pytest.mark.timeout(540)
 def test_reference_main_cpp_validates_every_case():
-    assert os.path.exists(BIN), "oracle/_ref/main_amd missing: build it with `make -C oracle harness`"
+    assert os.path.exists(BIN), "oracle/_ref/main_amd_rv missing: build it with `make -C oracle harness`"
     import tcsc_amd  # noqa: F401  (fails loudly without the library)
 
     sys.path.insert(0, os.path.join(PKG, "harness"))
@@ -52,6 +57,7 @@ def test_reference_main_cpp_validates_every_case():
 
     env = dict(os.environ)
     env.pop("TCSC_PATH", None)
+    env["TCSC_DENSE_THREADS"] = "0"  # the timing calls' gemm_basic on the box's cores
     live = None
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
         live = open(os.path.join(ROOT, "gpurun_out", "main_amd_out.txt"), "w", buffering=1)
@@ -116,6 +122,9 @@ def test_reference_main_cpp_validates_every_case():
     assert not errors, errors
     assert oks == len(CASES), f"{oks} of {len(CASES)} cases validated; rc={p.returncode}\n{out[-3000:]}"
     assert p.returncode == 0 and "ALL BENCHMARKS COMPLETED" in out, out[-3000:]
+    tag = "[harness_wrap] gemm_basic:"
+    report = [ln[ln.index(tag) + len(tag):].strip() for ln in lines if tag in ln]  # (after a progress bar)
+    assert report and report[-1].startswith(f"{len(CASES)} validation call(s) by the reference's"), report
     algos, cases = out2csv.parse(lines)
     assert [(c["M"], c["K"], c["N"]) for c in cases] == CASES
     for c in cases:

@@ -109,6 +109,10 @@ FDEF_dl := -DTCSC_PRODUCE_DELAY
 FDEF_nl := -DTCSC_FUSED_DIAG_NOLOOP=1
 FDEF_pu := -DTCSC_FUSED_DIAG_PURE=1
 FDEF_st := -DTCSC_FUSED_STAMPS=1
+FDEF_rr := -DTCSC_FUSED_XCD_RANGES=0
+FDEF_late := -DTCSC_FUSED_PROD_LATE=1
+FDEF_prio := -DTCSC_FUSED_PROD_PRIO=1
+FDEF_lp := -DTCSC_FUSED_PROD_LATE=1 -DTCSC_FUSED_PROD_PRIO=1
 lib/abl/libtcsc_amd_f%.so: $(SRC)/tcsc_kernels.hip $(SRC)/tcsc_api.cpp $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o $(HDRS) $(SRC)/gather_asm.inc
 	@mkdir -p lib/abl $(OBJ)/abl
 	$(HIPCC) $(HIPFLAGS) $(FDEF_$*) -c $(SRC)/tcsc_kernels.hip -o $(OBJ)/abl/k_f$*.o

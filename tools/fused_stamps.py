@@ -17,7 +17,8 @@ import tcsc_amd  # noqa: E402
 import torch  # noqa: E402
 
 SLOTS = ["prologue", "chunk loop", "epilogue", "producer steps", "blocking polls", "blocking poll count", "wave0 barrier waits",
-         "producer step count"]
+         "producer step count", "step: record read", "step: vmcnt wait", "step: slot read+stores", "step: DMA issue",
+         "step: signal"]
 
 
 def main(M=4096, K=16384, N=16384, density=0.02, reps=5):
@@ -42,11 +43,11 @@ def main(M=4096, K=16384, N=16384, density=0.02, reps=5):
     X = torch.randn((M, K), generator=g, device=dev)
     B = torch.zeros(N, device=dev)
     Y = torch.empty((M, N), device=dev)
-    buf = (C.c_ulonglong * (4096 * 8))()
+    buf = (C.c_ulonglong * (4096 * 16))()
     for _ in range(2):
         plan.sgemm(X, B, Y, M, N, "prelu_basic", 0.2)
     torch.cuda.synchronize()
-    lib.tcsc_diag_fused_stamps(buf, 4096 * 8)
+    lib.tcsc_diag_fused_stamps(buf, 4096 * 16)
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
     s.record()
@@ -55,8 +56,8 @@ def main(M=4096, K=16384, N=16384, density=0.02, reps=5):
     e.record()
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / reps
-    lib.tcsc_diag_fused_stamps(buf, 4096 * 8)
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8)
+    lib.tcsc_diag_fused_stamps(buf, 4096 * 16)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 16)
     used = a[:, 1] > 0
     a = a[used].astype(np.float64) / reps
     print(f"{ms:.3f} ms per launch, {used.sum()} workgroups, {plan.launch_info(M)}")
