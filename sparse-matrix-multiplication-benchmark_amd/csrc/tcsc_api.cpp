@@ -517,8 +517,6 @@ namespace {
 // The MFMA path (stage 0: all; 1: split only; 2: GEMM + fixup on the staged
 // X3): k_split3 (X -> X3 + row flags), k_gemm3 (Y = act(X3 . W3T^T + B),
 // the bias and PReLU in its store), k_fixup (the flagged rows, exact).
-// Stage 0 with K % 32 == 0 runs k_gemm3x instead (the split fused into the
-// GEMM's operand reads, flags from its column-tile-0 workgroups) + k_fixup_x.
 int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy, int variant,
                float a, void* stream, float* ws, size_t ws_bytes, int stage) {
     const int K = p->rows, N = p->cols, ldk = tcsc::mfma_ldk(K);
@@ -530,13 +528,6 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
     hipStream_t st = static_cast<hipStream_t>(stream);
     uint16_t* x3 = reinterpret_cast<uint16_t*>(ws);
     int* flags = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + align256((size_t)M * ldk * 2));
-    if (stage == 0 && tcsc::mfma_fused_ok(dX, K)) {  // one pass: the split inside the GEMM's operand reads
-        const bool prelu = is_prelu(variant);
-        HIP_TRY(tcsc::mfma_gemm3x(dX, p->w3, ldk, M, N, K, dB, dY, ldy, prelu, a, flags, st));
-        HIP_TRY(tcsc::mfma_fixup_x(dX, M, K, p->ccp, p->ccn, p->crp, p->crn, N, dB, dY, ldy,
-                                   variant == TCSC_VARIANT_BASIC, prelu, a, flags, st));
-        return TCSC_OK;
-    }
     if (stage != 2) HIP_TRY(tcsc::mfma_split_x(dX, M, K, x3, ldk, flags, st));
     if (stage == 1) return TCSC_OK;
     const bool prelu = is_prelu(variant);

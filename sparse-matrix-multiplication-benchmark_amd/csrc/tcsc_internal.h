@@ -314,9 +314,19 @@ hipError_t csc_copy(const int* csp, const int* csn, const int* rip, const int* r
                     long long n_pos, long long n_neg, int* cp, int* cn, int* crp, int* crn, hipStream_t st);
 
 // ---- MFMA path for near-dense W (tcsc_mfma.hip) ------------
-// X3 / W3T rows are ldk = mfma_ldk(K) bf16 long: [h | m | l] (X3) or
-// [w | w | w] (W3T), zero-padded to a multiple of the GEMM's 64-deep k step.
-inline int mfma_ldk(int K) { return (3 * K + 63) / 64 * 64; }
+// X3 / W3T rows are ldk = mfma_ldk(K) bf16 long, in blocks of kMfmaBlk = 32
+// k (one MFMA's depth): [h | m | l] of block 0, of block 1, ... (X3) or
+// [w | w | w] per block (W3T), zeros past K and up to a multiple of the
+// GEMM's 64-deep k step.  Each MFMA thus adds one part of one block, and the
+// accumulation runs k-major (h, m, l of a block, then the next block): its
+// fp32 rounding error is about half that of a part-major [h | m | l] image
+// (the accumulator is not carried across K three times).
+constexpr int kMfmaBlk = 32;
+__host__ __device__ inline int mfma_nblk(int K) { return (K + kMfmaBlk - 1) / kMfmaBlk; }
+__host__ __device__ inline int mfma_ldk(int K) { return (3 * kMfmaBlk * mfma_nblk(K) + 63) / 64 * 64; }
+__host__ __device__ inline int x3_index(int k, int part) {
+    return (k / kMfmaBlk) * (3 * kMfmaBlk) + part * kMfmaBlk + k % kMfmaBlk;
+}
 // Build: wf (ncols x rows fp32 scratch) <- the +1/-1 entries of columns
 // [col_begin, col_begin+ncols) (absolute offsets), transposed; w3 <- W^T
 // with three bf16 copies per row (ncols x ldk).  *bad = 1 if a weight is
@@ -333,13 +343,6 @@ hipError_t launch_small_m(const float* X, int M, int K, const int* cp, const int
 // X (M x K) -> x3 (M x ldk bf16, [h | m | l | 0..]); flags[m] = 1 for the
 // rows the fixup recomputes, 0 otherwise (every row, every call).
 hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int* flags, hipStream_t st);
-// the fused-split path (k_gemm3x + k_fixup_x): X read directly, no X3
-bool mfma_fused_ok(const float* X, int K);
-hipError_t mfma_gemm3x(const float* X, const uint16_t* w3, int ldk, int M, int N, int K, const float* B, float* Y,
-                       int ldy, bool prelu, float a, int* flags, hipStream_t st);
-hipError_t mfma_fixup_x(const float* X, int M, int K, const int* cp, const int* cn, const int* crp, const int* crn,
-                        int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
-                        const int* flags, hipStream_t st);
 // k_gemm3: Y = act(x3 . w3^T + B) on the matrix cores (bias after the sum).
 hipError_t mfma_gemm3(const uint16_t* x3, const uint16_t* w3, int ldk, int M, int N, const float* B, float* Y,
                       int ldy, bool prelu, float a, hipStream_t st);

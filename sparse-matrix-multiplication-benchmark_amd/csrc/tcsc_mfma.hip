@@ -29,8 +29,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <cstdlib>
-#include <type_traits>
 
 #include "tcsc_internal.h"
 
@@ -91,20 +89,23 @@ __global__ void __launch_bounds__(256) k_split3(const float* __restrict__ X, int
         }
         uint16_t h[4], m[4], l[4];
         for (int j = 0; j < 4; ++j) fix |= split3(v[j], h[j], m[j], l[j]);
-        if (vec) {
+        if (vec) {  // k0 .. k0+3 lie in one 32-k block
             typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
-            *reinterpret_cast<u16x4*>(dst + k0) = u16x4{h[0], h[1], h[2], h[3]};
-            *reinterpret_cast<u16x4*>(dst + K + k0) = u16x4{m[0], m[1], m[2], m[3]};
-            *reinterpret_cast<u16x4*>(dst + 2 * K + k0) = u16x4{l[0], l[1], l[2], l[3]};
+            *reinterpret_cast<u16x4*>(dst + x3_index(k0, 0)) = u16x4{h[0], h[1], h[2], h[3]};
+            *reinterpret_cast<u16x4*>(dst + x3_index(k0, 1)) = u16x4{m[0], m[1], m[2], m[3]};
+            *reinterpret_cast<u16x4*>(dst + x3_index(k0, 2)) = u16x4{l[0], l[1], l[2], l[3]};
         } else {
             for (int j = 0; j < 4 && k0 + j < K; ++j) {
-                dst[k0 + j] = h[j];
-                dst[K + k0 + j] = m[j];
-                dst[2 * K + k0 + j] = l[j];
+                dst[x3_index(k0 + j, 0)] = h[j];
+                dst[x3_index(k0 + j, 1)] = m[j];
+                dst[x3_index(k0 + j, 2)] = l[j];
             }
         }
     }
-    for (int k = 3 * K + threadIdx.x; k < ldk; k += blockDim.x) dst[k] = 0;
+    // zeros past K: the last block's tail in each part, then the row pad
+    const int tail0 = (mfma_nblk(K) - 1) * 3 * kMfmaBlk;
+    for (int i = tail0 + threadIdx.x; i < ldk; i += blockDim.x)
+        if (i >= 3 * kMfmaBlk * mfma_nblk(K) || (mfma_nblk(K) - 1) * kMfmaBlk + i % kMfmaBlk >= K) dst[i] = 0;
     fix = __syncthreads_or(fix);
     if (threadIdx.x == 0) flags[row] = fix ? 1 : 0;
 }
@@ -135,9 +136,9 @@ __global__ void k_w3_from(const float* __restrict__ WfT, int ncols, int K, uint1
         const uint16_t b = (uint16_t)(f2u(w) >> 16);
         const long long j = i / K, k = i - j * K;
         uint16_t* row = W3T + j * ldk;
-        row[k] = b;
-        row[K + k] = b;
-        row[2 * K + k] = b;
+        row[x3_index((int)k, 0)] = b;
+        row[x3_index((int)k, 1)] = b;
+        row[x3_index((int)k, 2)] = b;
     }
 }
 
@@ -160,7 +161,8 @@ __device__ inline float exact_out(const uint16_t* __restrict__ X3, int K, int ld
                                   float a) {
     const uint16_t* x3 = X3 + (size_t)row * ldk;
     auto xk = [&](int k) {
-        return (u2f((uint32_t)x3[k] << 16) + u2f((uint32_t)x3[K + k] << 16)) + u2f((uint32_t)x3[2 * K + k] << 16);
+        return (u2f((uint32_t)x3[x3_index(k, 0)] << 16) + u2f((uint32_t)x3[x3_index(k, 1)] << 16)) +
+               u2f((uint32_t)x3[x3_index(k, 2)] << 16);
     };
     float acc = BIAS_FIRST ? Bias[j] : 0.0f;
     int p = cp[j], q = cn[j];
@@ -331,229 +333,6 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
 }
 
 
-// ---------------------------------------------------------------------------
-// k_gemm3x: the same product with the split fused into the operand reads
-// (SparseGEMM.h:104-119's product, one pass over X): per k step of 32 the
-// workgroup stages X's fp32 tile and W^T's bf16 tile (the first K columns
-// of W3T) by LDS-DMA; each wave reads its A fragment as 8 fp32 per lane,
-// splits it into h, m, l in registers and issues three MFMAs per (i, j)
-// against one B fragment.  Against k_split3 + k_gemm3 this drops the X3
-// round trip (M x 3K bf16 written and read back) and stages W^T once per k
-// instead of three times; the sum runs k-major (h, m, l per k step) instead
-// of part-major, so float results differ in rounding (same bound; integer
-// inputs exact).  Needs K % 32 == 0 and 16-B aligned X rows.
-// * LDS image: A's rows in 1-KiB pieces of 8 rows x 32 fp32, B's in pieces
-//   of 16 rows x 32 bf16; 16-B granule g of row R (R: row in the 16-row
-//   fragment block) at slot 8R' + (g ^ swz_a(R)) resp. 4R + (g ^ swz_b(R)).
-//   The swizzle tables were searched (tools/lds_banks.py) so that every
-//   ds_read_b128 lane group of the fragment reads hits 16 distinct
-//   bank quads: conflict-free.
-// * Row flags (the fixup's input, as k_split3's) come from the column-tile-0
-//   workgroups' waves of column 0: non-finite or tiny nonzero x.
-// ---------------------------------------------------------------------------
-constexpr unsigned long long kSwzA = 0x5a040ba65b0dull;  // 3 bits per row R = 0..15
-constexpr unsigned kSwzB = 0x874825eau;                   // 2 bits per row R = 0..15
-__device__ inline int swz_a(int R) { return (int)((kSwzA >> (3 * R)) & 7); }
-__device__ inline int swz_b(int R) { return (int)((kSwzB >> (2 * R)) & 3); }
-
-// x = h + m + l exactly (finite x): bf16 bit patterns, two values per dword
-__device__ inline void split_pair(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
-    const uint32_t u0 = f2u(x0), u1 = f2u(x1);
-    const uint32_t h0 = u0 & 0xffff0000u, h1 = u1 & 0xffff0000u;
-    const float r0 = x0 - u2f(h0), r1 = x1 - u2f(h1);
-    const uint32_t m0 = f2u(r0) & 0xffff0000u, m1 = f2u(r1) & 0xffff0000u;
-    const float s0 = r0 - u2f(m0), s1 = r1 - u2f(m1);
-    h = h1 | (h0 >> 16);
-    m = m1 | (m0 >> 16);
-    l = (f2u(s1) & 0xffff0000u) | (f2u(s0) >> 16);
-}
-
-// Branch-free row-flag test (bit 31 set when x needs the fixup): with
-// a = |x| bits, non-finite <=> a + 2^23 >= 2^31, tiny nonzero <=>
-// 0 < a < bits(2^-100) = 27 << 23 (a - (27 << 23) negative and -a negative).
-__device__ inline uint32_t fixup_bit31(float x) {
-    const uint32_t a = f2u(x) & 0x7fffffffu;
-    return (a + 0x00800000u) | ((a - (27u << 23)) & (0u - a));
-}
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-template <int WM, int WN, int FI, int FJ, bool PRELU>
-__global__ void __launch_bounds__(WM * WN * 64) k_gemm3x(const float* __restrict__ X, int ldx,
-                                                       const uint16_t* __restrict__ Bt, int ldk, int M, int N,
-                                                       int ksteps, const float* __restrict__ bias,
-                                                       float* __restrict__ Y, int ldy, float a, int tiles_m,
-                                                       int tiles_n, int* __restrict__ flags) {
-    constexpr int TM = WM * FI * 16, TN = WN * FJ * 16, NW = WM * WN;
-    constexpr int PA = TM / 8, PB = TN / 16;  // 1-KiB pieces per stage
-    constexpr int STAGE = (PA + PB) * 1024;
-    constexpr int PPW = (PA + PB) / NW;
-    static_assert((PA + PB) % NW == 0, "whole pieces per wave");
-    static_assert(FI <= 32, "row flags in one dword");
-    __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];
-
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wr = wave / WN, wc = wave % WN;
-
-    const int T = tiles_m * tiles_n, L = blockIdx.x;
-    const int q = T >> 3, r = T & 7, x = L & 7;
-    const int Lg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
-    const int grp = Lg / (tiles_m * 4), idx = Lg % (tiles_m * 4);
-    const int tm = idx % tiles_m, tn = grp * 4 + idx / tiles_m;
-    const int m0 = tm * TM, n0 = tn * TN;
-
-    const char* src[PPW];
-    int stp[PPW], dst[PPW];
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-        const int piece = wave * PPW + i;
-        if (piece < PA) {
-            const int rr = lane >> 3, R = 8 * (piece & 1) + rr, g = (lane & 7) ^ swz_a(R);
-            const int row = min(m0 + 8 * piece + rr, M - 1);
-            src[i] = reinterpret_cast<const char*>(X + (size_t)row * ldx + 4 * g);
-            stp[i] = 32 * 4;
-        } else {
-            const int R = lane >> 2, g = (lane & 3) ^ swz_b(R);
-            const int row = min(n0 + 16 * (piece - PA) + R, N - 1);
-            src[i] = reinterpret_cast<const char*>(Bt + (size_t)row * ldk + 8 * g);
-            stp[i] = 32 * 2;
-        }
-        dst[i] = piece * 1024;
-    }
-    auto dma = [&](int kstep, int buf) {
-#pragma unroll
-        for (int i = 0; i < PPW; ++i)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + (size_t)kstep * stp[i]),
-                                             (__attribute__((address_space(3))) void*)(lds + buf * STAGE + dst[i]),
-                                             16, 0, 0);
-    };
-
-    const int R = lane & 15;
-    int aoff[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) aoff[h] = (R >> 3) * 1024 + 16 * (8 * (R & 7) + ((2 * (lane >> 4) + h) ^ swz_a(R)));
-    const int boff = 16 * (4 * R + ((lane >> 4) ^ swz_b(R)));
-
-    f32x4 acc[FI][FJ];
-#pragma unroll
-    for (int i = 0; i < FI; ++i)
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const bool do_flags = flags != nullptr && tn == 0 && wc == 0;
-    uint32_t fl = 0;
-
-    dma(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // the k loop, compiled twice: with the row-flag test (column-tile-0 waves
-    // of column 0) and without (everyone else: no extra VALU in the loop)
-    auto kloop = [&](auto flags_c) {
-    constexpr bool FLAGS = decltype(flags_c)::value;
-    for (int t = 0; t < ksteps; ++t) {
-        const int buf = t & 1;
-        if (t + 1 < ksteps) dma(t + 1, buf ^ 1);
-        const char* sb = lds + buf * STAGE;
-        bf16x8 bfr[FJ];
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(sb + (PA + wc * FJ + j) * 1024 + boff);
-#pragma unroll
-        for (int i = 0; i < FI; ++i) {
-            const char* ab = sb + (wr * FI + i) * 2048;
-            const f32x4 x0 = *reinterpret_cast<const f32x4*>(ab + aoff[0]);
-            const f32x4 x1 = *reinterpret_cast<const f32x4*>(ab + aoff[1]);
-            if constexpr (FLAGS) {
-                const uint32_t bad = fixup_bit31(x0.x) | fixup_bit31(x0.y) | fixup_bit31(x0.z) | fixup_bit31(x0.w) |
-                                     fixup_bit31(x1.x) | fixup_bit31(x1.y) | fixup_bit31(x1.z) | fixup_bit31(x1.w);
-                fl |= (bad >> 31) << i;
-            }
-            uint32_t h0, h1, h2, h3, mm0, mm1, mm2, mm3, l0, l1, l2, l3;
-            split_pair(x0.x, x0.y, h0, mm0, l0);
-            split_pair(x0.z, x0.w, h1, mm1, l1);
-            split_pair(x1.x, x1.y, h2, mm2, l2);
-            split_pair(x1.z, x1.w, h3, mm3, l3);
-            const u32x4 hv = {h0, h1, h2, h3}, mv = {mm0, mm1, mm2, mm3}, lv = {l0, l1, l2, l3};
-            const bf16x8 ah = __builtin_bit_cast(bf16x8, hv), am = __builtin_bit_cast(bf16x8, mv),
-                         al = __builtin_bit_cast(bf16x8, lv);
-            // part-major over j: an accumulator's next MFMA is FJ MFMAs away
-            // (back-to-back MFMAs on one accumulator stall on its latency)
-#pragma unroll
-            for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bfr[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-            for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bfr[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-            for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bfr[j], acc[i][j], 0, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    };
-    if (do_flags)
-        kloop(std::true_type{});
-    else
-        kloop(std::false_type{});
-
-    if (do_flags) {  // lanes l, l^16, l^32, l^48 hold row l & 15 of each block
-        fl |= (uint32_t)__shfl_xor((int)fl, 16);
-        fl |= (uint32_t)__shfl_xor((int)fl, 32);
-        if (lane < 16)
-#pragma unroll
-            for (int i = 0; i < FI; ++i) {
-                const int row = m0 + (wr * FI + i) * 16 + lane;
-                if (row < M) flags[row] = (fl >> i) & 1;
-            }
-    }
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-        const int col = n0 + (wc * FJ + j) * 16 + (lane & 15);
-        const float b = col < N ? bias[col] : 0.0f;
-#pragma unroll
-        for (int i = 0; i < FI; ++i) {
-            const int rowb = m0 + (wr * FI + i) * 16 + 4 * (lane >> 4);
-#pragma unroll
-            for (int rg = 0; rg < 4; ++rg) {
-                const int row = rowb + rg;
-                float v = acc[i][j][rg] + b;
-                if (PRELU) v = (v < 0.0f) ? a * v : v;
-                if (row < M && col < N) __builtin_nontemporal_store(v, Y + (size_t)row * ldy + col);
-            }
-        }
-    }
-}
-
-// k_fixup reading x from X itself (the fused path keeps no X3)
-template <bool BIAS_FIRST, bool PRELU>
-__global__ void __launch_bounds__(256) k_fixup_x(const float* __restrict__ X, int M, int K,
-                                                 const int* __restrict__ cp, const int* __restrict__ cn,
-                                                 const int* __restrict__ rp, const int* __restrict__ rn, int ncols,
-                                                 const float* __restrict__ Bias, float* __restrict__ Y, int ldy,
-                                                 float a, const int* __restrict__ flags) {
-    int any = 0;
-    for (int r = threadIdx.x; r < M; r += blockDim.x) any |= flags[r];
-    if (!__syncthreads_or(any)) return;
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= ncols) return;
-    for (int row = 0; row < M; ++row) {
-        if (!flags[row]) continue;
-        const float* xr = X + (size_t)row * K;
-        float acc = BIAS_FIRST ? Bias[j] : 0.0f;
-        int p = cp[j], q = cn[j];
-        const int p1 = cp[j + 1], q1 = cn[j + 1];
-        while (p < p1 || q < q1) {
-            if (q >= q1 || (p < p1 && rp[p] <= rn[q])) {
-                acc = fmaf(xr[rp[p]], 1.0f, acc);
-                ++p;
-            } else {
-                acc = fmaf(xr[rn[q]], -1.0f, acc);
-                ++q;
-            }
-        }
-        if (!BIAS_FIRST) acc += Bias[j];
-        if (PRELU) acc = (acc < 0.0f) ? a * acc : acc;
-        Y[(size_t)row * ldy + j] = acc;
-    }
-}
-
 }  // namespace
 
 hipError_t csc_copy(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int ncols,
@@ -634,58 +413,6 @@ hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cp, 
             hipLaunchKernelGGL((k_fixup<false, true>), grid, block, 0, st, TCSC_FIX_ARGS);
         else
             hipLaunchKernelGGL((k_fixup<false, false>), grid, block, 0, st, TCSC_FIX_ARGS);
-    }
-#undef TCSC_FIX_ARGS
-    return hipGetLastError();
-}
-
-// TCSC_MFMA_FUSED=0 keeps the split + GEMM pair (A/B and regression checks)
-bool mfma_fused_ok(const float* X, int K) {
-    const char* v = std::getenv("TCSC_MFMA_FUSED");
-    const int on = v && *v ? std::atoi(v) : 0;  // opt-in until validated on the GPU
-    return on != 0 && K > 0 && K % 32 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
-}
-
-template <bool PRELU>
-static hipError_t launch_gemm3x_t(const float* X, const uint16_t* w3, int ldk, int M, int N, int K, const float* B,
-                                  float* Y, int ldy, float a, int* flags, hipStream_t st) {
-    const int ksteps = K / 32;
-    const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
-    if (big >= 128) {
-        const int tm = (M + 255) / 256, tn = (N + 255) / 256;
-        hipLaunchKernelGGL((k_gemm3x<2, 4, 8, 4, PRELU>), dim3(tm * tn), dim3(512), 0, st, X, K, w3, ldk, M, N,
-                           ksteps, B, Y, ldy, a, tm, tn, flags);
-    } else {
-        const int tm = (M + 127) / 128, tn = (N + 127) / 128;
-        hipLaunchKernelGGL((k_gemm3x<2, 2, 4, 4, PRELU>), dim3(tm * tn), dim3(256), 0, st, X, K, w3, ldk, M, N,
-                           ksteps, B, Y, ldy, a, tm, tn, flags);
-    }
-    return hipGetLastError();
-}
-
-hipError_t mfma_gemm3x(const float* X, const uint16_t* w3, int ldk, int M, int N, int K, const float* B, float* Y,
-                       int ldy, bool prelu, float a, int* flags, hipStream_t st) {
-    if (M <= 0 || N <= 0) return hipSuccess;
-    if (K % 32 != 0 || ldk % 64 != 0) return hipErrorInvalidValue;
-    return prelu ? launch_gemm3x_t<true>(X, w3, ldk, M, N, K, B, Y, ldy, a, flags, st)
-                 : launch_gemm3x_t<false>(X, w3, ldk, M, N, K, B, Y, ldy, a, flags, st);
-}
-
-hipError_t mfma_fixup_x(const float* X, int M, int K, const int* cp, const int* cn, const int* crp, const int* crn,
-                        int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
-                        const int* flags, hipStream_t st) {
-    const dim3 grid((ncols + 255) / 256), block(256);
-#define TCSC_FIX_ARGS X, M, K, cp, cn, crp, crn, ncols, B, Y, ldy, a, flags
-    if (bias_first) {
-        if (prelu)
-            hipLaunchKernelGGL((k_fixup_x<true, true>), grid, block, 0, st, TCSC_FIX_ARGS);
-        else
-            hipLaunchKernelGGL((k_fixup_x<true, false>), grid, block, 0, st, TCSC_FIX_ARGS);
-    } else {
-        if (prelu)
-            hipLaunchKernelGGL((k_fixup_x<false, true>), grid, block, 0, st, TCSC_FIX_ARGS);
-        else
-            hipLaunchKernelGGL((k_fixup_x<false, false>), grid, block, 0, st, TCSC_FIX_ARGS);
     }
 #undef TCSC_FIX_ARGS
     return hipGetLastError();

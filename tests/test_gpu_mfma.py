@@ -88,41 +88,6 @@ def test_float_within_bound_all_variants(gpu, oracle, path, K):
     W.free()
 
 
-@pytest.mark.parametrize("fused", ["1", "0"])
-def test_fused_split_gemm_and_two_pass_path_hold_the_same_bars(gpu, oracle, path, monkeypatch, fused):
-    """K % 32 == 0 runs k_gemm3x (the split inside the GEMM's operand reads,
-    TCSC_MFMA_FUSED=1, the default) or k_split3 + k_gemm3 (=0): both within
-    the float bound, both bit-exact on integer inputs, the same flagged rows."""
-    monkeypatch.setenv("TCSC_MFMA_FUSED", fused)
-    monkeypatch.setenv("TCSC_SLICES", "1")  # the gather without split-K: the fixup's order
-    path(None)
-    M, K, N = 300, 1024, 520
-    Wd, X, B = float_case(oracle, M, K, N, 0.5, 61)
-    X[7, 3] = np.inf
-    X[290, 1000] = np.float32(1e-40)
-    W = tcsc_amd.TcscMatrix.from_dense(Wd)
-    Wref = oracle.tcsc_from_dense(Wd)
-    rest = np.setdiff1d(np.arange(M), [7, 290])
-    Y64, S64 = oracle.f64_rows(X[rest], Wref, B)
-    Xi, Bi = oracle.integers((M, K), 62), oracle.integers((N,), 63)
-    for variant in ("prelu_basic", "basic"):
-        Y, info = device_run(W, X, B, variant)
-        assert info["mfma_min_M"] == 64
-        ok, ratio = pyoracle.check_close(Y[rest], Y64, S64, 0.2 if variant in pyoracle.PRELU_VARIANTS else None)
-        assert ok, f"{variant}: worst err/bound {ratio:.3g}"
-        path("gather")
-        Yg, _ = device_run(W, X, B, variant)
-        path(None)
-        for r in (7, 290):
-            g_, m_ = Yg[r], Y[r]
-            assert np.array_equal(np.isnan(g_), np.isnan(m_)), (variant, r)
-            fin = ~np.isnan(g_)
-            np.testing.assert_array_equal(m_[fin].view(np.uint32), g_[fin].view(np.uint32), err_msg=f"{variant} {r}")
-        Yi, _ = device_run(W, Xi, Bi, variant)
-        np.testing.assert_array_equal(Yi, oracle.sgemm(variant, Xi, Wref, Bi, 0.2), err_msg=variant)
-    W.free()
-
-
 def test_integer_inputs_bit_exact(gpu, oracle, path):
     path(None)
     M, K, N = 130, 512, 257
