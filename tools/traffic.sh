@@ -15,7 +15,7 @@ for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d gpurun_out/traffic$i -o run -- $B > gpurun_out/traffic$i.log 2>&1
   rc=$?; echo "pass $i ($set) rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
-ABL=$PWD/sparse-matrix-multiplication-benchmark_amd/lib/abl/libtcsc_amd_abl0_nd.so
+ABL=${ABL_LIB:-$PWD/sparse-matrix-multiplication-benchmark_amd/lib/abl/libtcsc_amd_abl0_nd.so}
 rm -rf gpurun_out/traffic4
 TCSC_AMD_LIB=$ABL timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/traffic4 -o run -- $B --no-validate > gpurun_out/traffic4.log 2>&1
 rc=$?; echo "pass 4 (FETCH_SIZE, no-DMA ablation) rc=$rc"; [ $rc -ne 0 ] && exit $rc
