@@ -294,45 +294,6 @@ __global__ void __launch_bounds__(256) k_transpose(const float* __restrict__ X, 
     }
 }
 
-// The same transpose with 256 (m) x 32 (k) tiles: one 128-B line per X row
-// read, 1-KiB contiguous X^T row pieces written (the 64 x 128 tile writes
-// 256-B pieces 16 KiB apart).  Row stride 33 keeps the column reads
-// conflict-free.  Needs K % 4 == 0 and 16-B aligned X (the VEC case).
-__global__ void __launch_bounds__(256) k_transpose_wide(const float* __restrict__ X, int M, int K,
-                                                        float* __restrict__ XT, int ldxt) {
-    __shared__ float tv[256][33];
-    const int k0 = blockIdx.x * 32, m0 = blockIdx.y * 256;
-    const int q = threadIdx.x & 7, r = threadIdx.x >> 3;  // 8 float4 per 32-wide row, 32 rows per pass
-    float4 v[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int m = m0 + r + 32 * i, k = k0 + 4 * q;
-        v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (m < M && k < K) {
-            typedef float nt4 __attribute__((ext_vector_type(4)));
-            const nt4 w = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(X + (size_t)m * K + k));
-            v[i] = make_float4(w.x, w.y, w.z, w.w);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int rr = r + 32 * i;
-        tv[rr][4 * q + 0] = v[i].x;
-        tv[rr][4 * q + 1] = v[i].y;
-        tv[rr][4 * q + 2] = v[i].z;
-        tv[rr][4 * q + 3] = v[i].w;
-    }
-    __syncthreads();
-    const int mq = threadIdx.x & 63, kr = threadIdx.x >> 6;  // 64 float4 per 256-wide X^T row piece
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int kk = kr + 4 * i, k = k0 + kk;
-        if (k < K)
-            *reinterpret_cast<float4*>(XT + (size_t)k * ldxt + m0 + 4 * mq) =
-                make_float4(tv[4 * mq + 0][kk], tv[4 * mq + 1][kk], tv[4 * mq + 2][kk], tv[4 * mq + 3][kk]);
-    }
-}
-
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(4))) const i32x16 const_i32x16;
 // the scalar buffer's last, 4- or 8-SGPR piece (header + CAP entries is not
@@ -2081,10 +2042,7 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
         if (!g.XT) return hipErrorInvalidValue;
         const int ldxt = ldxt_of(g.M);
         const bool vec = (g.K % 4 == 0) && ((reinterpret_cast<uintptr_t>(g.X) & 15) == 0);
-        if (vec && env_int("TCSC_XT_WIDE", 0))
-            hipLaunchKernelGGL(k_transpose_wide, dim3((g.K + 31) / 32, ldxt / 256), dim3(256), 0, st, g.X, g.M, g.K,
-                               g.XT, ldxt);
-        else if (vec)
+        if (vec)
             hipLaunchKernelGGL(k_transpose<true>, dim3((g.K + 127) / 128, ldxt / 64), dim3(256), 0, st, g.X, g.M, g.K,
                                g.XT, ldxt);
         else
