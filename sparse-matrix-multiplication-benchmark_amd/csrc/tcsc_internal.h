@@ -179,24 +179,14 @@ constexpr int kPollWave = 6;                     // polls the piece counters
 static_assert(kProdWave0 >= kDmaWaves && kPollWave >= kDmaWaves, "producer and poll waves issue no ring DMAs");
 // LDS: the ring, one 256-B landing area that every wave's stream prefetch
 // shares (the data is never read), the producer slots, the item record
-#ifndef TCSC_FUSED_PF_LAST
-#define TCSC_FUSED_PF_LAST 0
-#endif
 constexpr int kFusedStateBytes = 128;  // item record (64 B) + producer states (16 B each) + 8 probe words
 constexpr int kProbeAhead = 4;         // chunks between a counter's probe and its check
 constexpr int kStoreDelay = 2;         // chunks from a unit's LDS-DMA to its stores
 constexpr int kSigDelay = 3;           // chunks from a unit's stores to its signal
-#if TCSC_FUSED_PF_LAST
-constexpr int kFusedSlotOff = kRingBytes;
-constexpr int kFusedStateOff = kFusedSlotOff + kProdWaves * kUnitBytes;
-constexpr int kFusedPfOff = kFusedStateOff + kFusedStateBytes;
-constexpr int kFusedLdsBytes0 = kFusedPfOff + 256;
-#else
 constexpr int kFusedPfOff = kRingBytes;
 constexpr int kFusedSlotOff = kFusedPfOff + 256;
 constexpr int kFusedStateOff = kFusedSlotOff + kProdWaves * kUnitBytes;
 constexpr int kFusedLdsBytes0 = kFusedStateOff + kFusedStateBytes;
-#endif
 constexpr int kFusedProbeOff = kFusedStateOff + 96;
 constexpr int kFusedLdsBytes = kFusedLdsBytes0 > kEpiMinBytes ? kFusedLdsBytes0 : kEpiMinBytes;
 static_assert(kFusedLdsBytes <= 160 * 1024, "fused kernel LDS");

@@ -832,6 +832,7 @@ __device__ unsigned long long g_fstamp[4096 * 16];
 #define FST_NOW() 0ull
 #define FST_ADD(lds, slot, v) \
     do {                      \
+        (void)(v);            \
     } while (0)
 #endif
 
@@ -920,14 +921,11 @@ __device__ __forceinline__ void unit_dma(const float* X, int K, int M, int m0, i
 #pragma unroll
     for (int r = 0; r < 4; ++r) off[r] = (unsigned)min(4 * lane + r, mmax) * (unsigned)K * 4u;
     unsigned sv;
-#ifndef TCSC_UNIT_NOP
-#define TCSC_UNIT_NOP "0"
-#endif
     asm volatile("s_mov_b32 %[sv], m0\n\t"
-                 "s_mov_b32 m0, %[s0]\n\ts_nop " TCSC_UNIT_NOP "\n\tglobal_load_lds_dwordx4 %[o0], %[b]\n\t"
-                 "s_add_u32 m0, m0, 0x400\n\ts_nop " TCSC_UNIT_NOP "\n\tglobal_load_lds_dwordx4 %[o1], %[b]\n\t"
-                 "s_add_u32 m0, m0, 0x400\n\ts_nop " TCSC_UNIT_NOP "\n\tglobal_load_lds_dwordx4 %[o2], %[b]\n\t"
-                 "s_add_u32 m0, m0, 0x400\n\ts_nop " TCSC_UNIT_NOP "\n\tglobal_load_lds_dwordx4 %[o3], %[b]\n\t"
+                 "s_mov_b32 m0, %[s0]\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o0], %[b]\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o1], %[b]\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o2], %[b]\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o3], %[b]\n\t"
                  "s_mov_b32 m0, %[sv]"
                  : [sv] "=&s"(sv)
                  : [s0] "s"(slot), [o0] "v"(off[0]), [o1] "v"(off[1]), [o2] "v"(off[2]), [o3] "v"(off[3]),

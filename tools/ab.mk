@@ -100,12 +100,11 @@ lib/abl/libtcsc_amd_pfs%.so: $(SRC)/tcsc_kernels.hip $(SRC)/tcsc_api.cpp $(OBJ)/
 	$(HIPCC) $(HIPFLAGS) -DTCSC_PF_S=$* -c $(SRC)/tcsc_api.cpp -o $(OBJ)/abl/a_pfs$*.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)/abl/k_pfs$*.o $(OBJ)/abl/a_pfs$*.o $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o -lpthread -L$(ROCM)/lib -lrocblas -Wl,-rpath,$(ROCM)/lib
 
-# fused-kernel diagnostics: lib/abl/libtcsc_amd_fpf.so (stream-prefetch landing area after the
-# producer slots), lib/abl/libtcsc_amd_fnop.so (s_nop 4 after every M0 write of a unit's LDS-DMA)
-FDEF_pf := -DTCSC_FUSED_PF_LAST=1
-FDEF_nop := -DTCSC_UNIT_NOP='"4"'
-FDEF_w0 := -DTCSC_PRODUCE_WAIT0
-FDEF_dl := -DTCSC_PRODUCE_DELAY
+# k_fused timing variants (DESIGN.md §4 k_fused; nl gives wrong results, the others are
+# correct): lib/abl/libtcsc_amd_f<v>.so with v =
+#   nl  no in-loop production or polls (timing only)   pu  k_transpose + the gather, no production
+#   st  s_memtime stamps (tools/fused_stamps.py)        rr  round-robin item order
+#   late / prio / lp  producer steps after the gather / at raised priority / both
 FDEF_nl := -DTCSC_FUSED_DIAG_NOLOOP=1
 FDEF_pu := -DTCSC_FUSED_DIAG_PURE=1
 FDEF_st := -DTCSC_FUSED_STAMPS=1
