@@ -173,13 +173,20 @@ constexpr int kUnitK = 4;                        // k rows per transposition uni
 constexpr int kUnitsPerChunk = kTK / kUnitK;     // 12
 constexpr int kUnitBytes = kTM * kUnitK * 4;     // 4 KiB of LDS staging per unit
 static_assert(kTK % kUnitK == 0, "whole units per chunk");
-constexpr int kProdWave0 = 4;                    // producer waves 4, 5 (one LDS slot each)
-constexpr int kProdWaves = 2;
-constexpr int kPollWave = 6;                     // polls the piece counters
+// producer waves 4 .. 4+kProdWaves-1 (one LDS slot each; SIMD rank 1, which
+// has ~600 cycles of slack per chunk at the barrier), then the
+// wave that polls the piece counters
+#ifndef TCSC_FUSED_PROD_WAVES
+#define TCSC_FUSED_PROD_WAVES 3
+#endif
+constexpr int kProdWave0 = 4;
+constexpr int kProdWaves = TCSC_FUSED_PROD_WAVES;
+constexpr int kPollWave = kProdWave0 + kProdWaves;
+static_assert(kProdWaves >= 1 && kPollWave < 8, "producer and poll waves in SIMD rank 1");
 static_assert(kProdWave0 >= kDmaWaves && kPollWave >= kDmaWaves, "producer and poll waves issue no ring DMAs");
 // LDS: the ring, one 256-B landing area that every wave's stream prefetch
 // shares (the data is never read), the producer slots, the item record
-constexpr int kFusedStateBytes = 128;  // item record (64 B) + producer states (16 B each) + 8 probe words
+constexpr int kFusedStateBytes = 64 + 16 * kProdWaves + 32;  // item record, producer hand-over words, 8 probe words
 constexpr int kProbeAhead = 4;         // chunks between a counter's probe and its check
 constexpr int kStoreDelay = 2;         // chunks from a unit's LDS-DMA to its stores
 constexpr int kSigDelay = 3;           // chunks from a unit's stores to its signal
@@ -187,7 +194,7 @@ constexpr int kFusedPfOff = kRingBytes;
 constexpr int kFusedSlotOff = kFusedPfOff + 256;
 constexpr int kFusedStateOff = kFusedSlotOff + kProdWaves * kUnitBytes;
 constexpr int kFusedLdsBytes0 = kFusedStateOff + kFusedStateBytes;
-constexpr int kFusedProbeOff = kFusedStateOff + 96;
+constexpr int kFusedProbeOff = kFusedStateOff + 64 + 16 * kProdWaves;
 constexpr int kFusedLdsBytes = kFusedLdsBytes0 > kEpiMinBytes ? kFusedLdsBytes0 : kEpiMinBytes;
 static_assert(kFusedLdsBytes <= 160 * 1024, "fused kernel LDS");
 // synchronisation block of a plan (device memory, zeroed once): [0] the

@@ -848,6 +848,9 @@ __device__ __forceinline__ int xcd_slot(int b, int P) {
 // one XCD's L2 across rounds, as k_stream's tile order keeps them.  The
 // other schedule deals item slot + r*P (a group's items in one round, but
 // split over two XCDs, each reading the row tile into its own L2).
+#ifndef TCSC_FUSED_ONE_ACTION  // A/B: at most one stage (signal, store or DMA) per producer step
+#define TCSC_FUSED_ONE_ACTION 1
+#endif
 #ifndef TCSC_FUSED_PROD_LATE  // A/B: producer steps after the gather instead of after the barrier
 #define TCSC_FUSED_PROD_LATE 0
 #endif
@@ -1076,9 +1079,17 @@ __device__ __forceinline__ int produce_step(char* lds, int wave, int lane, int t
     const char* slot_ptr = lds + kFusedSlotOff + (wave - kProdWave0) * kUnitBytes;
     const unsigned long long q1 = FST_NOW();
     const bool sig_now = ps.s_u >= 0 && (drain || t >= ps.tS + kSigDelay);
-    const bool store_now = ps.d_u >= 0 && (ps.s_u < 0 || sig_now) && (drain || t >= ps.tD + kStoreDelay);
-    const bool dma_now = (ps.d_u < 0 || store_now) && ps.u_next < r.U &&
-                         (drain || t >= ((ps.u_next / r.upc - r.lead) << r.pcs));
+    bool store_now = ps.d_u >= 0 && (ps.s_u < 0 || sig_now) && (drain || t >= ps.tD + kStoreDelay);
+    bool dma_now = (ps.d_u < 0 || store_now) && ps.u_next < r.U &&
+                   (drain || t >= ((ps.u_next / r.upc - r.lead) << r.pcs));
+#if TCSC_FUSED_ONE_ACTION
+    // one stage per step (a step then fits the wave's slack at the barrier):
+    // the signal first, then the store, then the DMA
+    if (!drain) {
+        if (sig_now) store_now = false;
+        if (sig_now || store_now) dma_now = false;
+    }
+#endif
     if (!sig_now && !store_now && !dma_now) return prod_next_t(ps, r.U, r.upc, r.lead, r.pcs, t);
     // A signal needs this wave's stores complete: vmcnt(0) (the guide's
     // hand-off rule); they are >= kSigDelay chunks old, so it waits at most
@@ -1281,7 +1292,7 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
             int u_next = agent;
             if (agent >= 0) {
                 const int lead_units = min(U, lead * upc);
-                constexpr int half = kRingBytes / 2 / kUnitBytes;  // ring slots per producer wave
+                constexpr int half = kRingBytes / kProdWaves / kUnitBytes;  // ring slots per producer wave
                 const int slot0 = (wave - kProdWave0) * half * kUnitBytes;
                 while (u_next < lead_units) {
                     int nb = 0;
