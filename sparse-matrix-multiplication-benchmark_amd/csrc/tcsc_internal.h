@@ -166,23 +166,44 @@ struct PlanOut {
 // X^T is written by the same launch that gathers from it: the output tiles
 // (row tile rt, K slice z, column block cb) are items of a persistent grid,
 // grouped by (rt, z); the group's workgroups transpose its rows of X in
-// units of 4 k rows x 256 m (one LDS-DMA of 4 x 1 KiB, four 1-KiB stores)
-// a few pieces ahead of their own gather, and signal per piece of
-// kFusedPieceChunks chunks on a counter {epoch, count}.
+// units a few pieces ahead of their own gather and count per piece of pc
+// chunks.  Two unit geometries (TCSC_FUSED_SMALL):
+//  * 0 (default): 4 k rows x 256 m (LDS-DMA of 4 x 1 KiB, 4 x 4 transpose in
+//    registers, four 1-KiB stores), one unit per step, made by waves 4-6;
+//  * 1: 1 k row x 64 m (one LDS-DMA dword per lane: 64 X rows, one
+//    ds_read_b32 and one 256-B store), batches of kSlotUnits per step, made
+//    by the 12 non-DMA waves 4-15, so that each wave's share per chunk is
+//    small.  Measured slower (cfg 4 1.84 against 1.46 ms: 16x the units,
+//    each as dear to issue), kept as an A/B build.
+#ifndef TCSC_FUSED_SMALL
+#define TCSC_FUSED_SMALL 0
+#endif
+#if TCSC_FUSED_SMALL
+constexpr int kUnitM = 64;                           // m per unit
+constexpr int kUnitsPerRow = kTM / kUnitM;           // 4 units per k row
+constexpr int kUnitsPerChunk = kTK * kUnitsPerRow;   // 192
+constexpr int kUnitBytes = kUnitM * 4;               // 256 B
+constexpr int kSlotUnits = 4;                        // units per producer step
+#ifndef TCSC_FUSED_PROD_WAVES
+#define TCSC_FUSED_PROD_WAVES 12
+#endif
+#else
 constexpr int kUnitK = 4;                        // k rows per transposition unit
 constexpr int kUnitsPerChunk = kTK / kUnitK;     // 12
 constexpr int kUnitBytes = kTM * kUnitK * 4;     // 4 KiB of LDS staging per unit
+constexpr int kSlotUnits = 1;
 static_assert(kTK % kUnitK == 0, "whole units per chunk");
-// producer waves 4 .. 4+kProdWaves-1 (one LDS slot each; SIMD rank 1, which
-// has ~600 cycles of slack per chunk at the barrier), then the
-// wave that polls the piece counters
 #ifndef TCSC_FUSED_PROD_WAVES
 #define TCSC_FUSED_PROD_WAVES 3
 #endif
+#endif
+// producer waves 4 .. 4+kProdWaves-1 (never the ring's DMA waves: the chunk
+// loop's vmcnt counts assume their VMEM ops); the poll wave is the first
+// producer in the small-unit geometry, the wave after the producers otherwise
 constexpr int kProdWave0 = 4;
 constexpr int kProdWaves = TCSC_FUSED_PROD_WAVES;
-constexpr int kPollWave = kProdWave0 + kProdWaves;
-static_assert(kProdWaves >= 1 && kPollWave < 8, "producer and poll waves in SIMD rank 1");
+constexpr int kPollWave = TCSC_FUSED_SMALL ? kProdWave0 : kProdWave0 + kProdWaves;
+static_assert(kProdWaves >= 1 && kProdWave0 + kProdWaves <= kWaves && kPollWave < kWaves, "producer and poll waves");
 static_assert(kProdWave0 >= kDmaWaves && kPollWave >= kDmaWaves, "producer and poll waves issue no ring DMAs");
 // LDS: the ring, one 256-B landing area that every wave's stream prefetch
 // shares (the data is never read), the producer slots, the item record
@@ -192,7 +213,7 @@ constexpr int kStoreDelay = 2;         // chunks from a unit's LDS-DMA to its st
 constexpr int kSigDelay = 3;           // chunks from a unit's stores to its signal
 constexpr int kFusedPfOff = kRingBytes;
 constexpr int kFusedSlotOff = kFusedPfOff + 256;
-constexpr int kFusedStateOff = kFusedSlotOff + kProdWaves * kUnitBytes;
+constexpr int kFusedStateOff = kFusedSlotOff + kProdWaves * kSlotUnits * kUnitBytes;
 constexpr int kFusedLdsBytes0 = kFusedStateOff + kFusedStateBytes;
 constexpr int kFusedProbeOff = kFusedStateOff + 64 + 16 * kProdWaves;
 constexpr int kFusedLdsBytes = kFusedLdsBytes0 > kEpiMinBytes ? kFusedLdsBytes0 : kEpiMinBytes;

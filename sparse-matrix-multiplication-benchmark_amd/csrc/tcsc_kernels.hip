@@ -993,6 +993,59 @@ __device__ __forceinline__ void unit_direct(const float* X, int K, int M, float*
     store4_sc1(base, o, st, r0, r1, r2, r3);
 }
 
+// Unit u of an item (relative to the item's first k row k_lo), on the row
+// tile's X rows (Xr = X + m0*K, mmax = M-1-m0) and X^T columns (XTr = XT + m0).
+#if TCSC_FUSED_SMALL
+// Small units: k row k_lo + u/4, columns 64*(u%4) .. +63 of the row tile.
+// LDS-DMA: lane l loads X[64q + l][k] (one dword) to slot + 4l; store: the
+// 64 dwords as one 256-B X^T row piece (sc1; a 4-B store has no data hazard).
+__device__ __forceinline__ void unit_dma_u(const float* Xr, int K, int mmax, int k_lo, int u, unsigned slot,
+                                           int lane) {
+    const int k = k_lo + (u >> 2), q = u & 3;
+    const char* base = reinterpret_cast<const char*>(Xr + k);
+    const unsigned off = (unsigned)min(64 * q + lane, mmax) * (unsigned)K * 4u;
+    unsigned sv;
+    asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %[s0]\n\ts_nop 0\n\tglobal_load_lds_dword %[o], %[b]\n\t"
+                 "s_mov_b32 m0, %[sv]"
+                 : [sv] "=&s"(sv)
+                 : [s0] "s"(slot), [o] "v"(off), [b] "s"(base)
+                 : "memory");
+}
+__device__ __forceinline__ void unit_store_u(const char* slot, float* XTr, int ldxt, int k_lo, int u, int lane) {
+    const int k = k_lo + (u >> 2), q = u & 3;
+    const float v = reinterpret_cast<const float*>(slot)[lane];
+    char* dst = reinterpret_cast<char*>(XTr + (size_t)k * ldxt + 64 * q);
+    asm volatile("global_store_dword %0, %1, %2 sc1" ::"v"(4u * (unsigned)lane), "v"(v), "s"(dst) : "memory");
+}
+__device__ __forceinline__ void unit_direct_u(const float* Xr, int K, int mmax, float* XTr, int ldxt, int k_lo, int u,
+                                              int lane) {
+    const int k = k_lo + (u >> 2), q = u & 3;
+    const float v = Xr[(size_t)min(64 * q + lane, mmax) * K + k];
+    char* dst = reinterpret_cast<char*>(XTr + (size_t)k * ldxt + 64 * q);
+    asm volatile("global_store_dword %0, %1, %2 sc1" ::"v"(4u * (unsigned)lane), "v"(v), "s"(dst) : "memory");
+}
+#else
+__device__ __forceinline__ void unit_dma_u(const float* Xr, int K, int mmax, int k_lo, int u, unsigned slot,
+                                           int lane) {
+    unit_dma(Xr + k_lo + kUnitK * u, K, mmax + 1, 0, 0, slot, lane);
+}
+__device__ __forceinline__ void unit_store_u(const char* slot, float* XTr, int ldxt, int k_lo, int u, int lane) {
+    unit_store(slot, XTr + (size_t)(k_lo + kUnitK * u) * ldxt, ldxt, 0, 0, lane);
+}
+__device__ __forceinline__ void unit_direct_u(const float* Xr, int K, int mmax, float* XTr, int ldxt, int k_lo, int u,
+                                              int lane) {
+    unit_direct(Xr + k_lo + kUnitK * u, K, mmax + 1, XTr + (size_t)(k_lo + kUnitK * u) * ldxt, ldxt, 0, 0, lane);
+}
+#endif
+// units of the k rows [k_lo, k_hi)
+__host__ __device__ constexpr int units_of(int krows) {
+#if TCSC_FUSED_SMALL
+    return krows * kUnitsPerRow;
+#else
+    return (krows + kUnitK - 1) / kUnitK;
+#endif
+}
+
 // The kernel's arguments, re-read from the kernarg segment at each use
 // (s_load, scalar-cache hits): an opaque copy of the segment pointer keeps
 // the compiler from holding every field in SGPRs across the chunk loop, where
@@ -1045,9 +1098,9 @@ __device__ __forceinline__ ItemRec load_rec(const char* lds) {
 }
 
 // One production step of a producer wave, at chunk t of the item (relative
-// to its first chunk).  An agent's units move through three stages, one unit
-// per stage at a time (ProdState, in registers: next unit, the unit in the
-// LDS slot and when its DMA was issued, the unit stored and when):
+// to its first chunk).  An agent's units move through three stages in batches
+// of kSlotUnits (ProdState, in registers: next unit, the batch in the LDS
+// slot and when its DMA was issued, the batch stored and when):
 //   DMA: unit u of piece p is issued once t >= (p - lead) * pc, i.e. about
 //        lead pieces ahead of the chunk that polls p -- production keeps a
 //        fixed distance ahead of the gather instead of racing it (racing
@@ -1062,7 +1115,11 @@ __device__ __forceinline__ ItemRec load_rec(const char* lds) {
 // next chunk at which a stage can move (the caller skips the step until
 // then: no LDS read per chunk), INT_MAX once the wave has nothing left.
 struct ProdState {
-    int u_next, d_u, s_u, tD, tS;  // next unit (INT_MAX: none), unit in the slot, unit stored (-1: none)
+    int u_next;    // the agent's next unit (INT_MAX: none left)
+    int d_u, d_n;  // first unit and count of the batch in the LDS slot (d_u -1: none)
+    int s_u, s_n;  // first unit and count of the batch stored, not yet signalled
+    int tD, tS;    // chunks of the batch's DMA and stores
+    int pf_n;      // stream prefetches issued since the last DMA (saturates at kStoreDelay)
 };
 
 __device__ __forceinline__ int prod_next_t(const ProdState& ps, int U, int upc, int lead, int pcs, int t) {
@@ -1076,7 +1133,7 @@ __device__ __forceinline__ int prod_next_t(const ProdState& ps, int U, int upc, 
 __device__ __forceinline__ int produce_step(char* lds, int wave, int lane, int t, bool drain, ProdState& ps,
                                             const ItemRec& r) {
     if (ps.u_next == 0x7fffffff && ps.d_u < 0 && ps.s_u < 0) return 0x7fffffff;
-    const char* slot_ptr = lds + kFusedSlotOff + (wave - kProdWave0) * kUnitBytes;
+    const char* slot_ptr = lds + kFusedSlotOff + (wave - kProdWave0) * (kSlotUnits * kUnitBytes);
     const unsigned long long q1 = FST_NOW();
     const bool sig_now = ps.s_u >= 0 && (drain || t >= ps.tS + kSigDelay);
     bool store_now = ps.d_u >= 0 && (ps.s_u < 0 || sig_now) && (drain || t >= ps.tD + kStoreDelay);
@@ -1092,42 +1149,64 @@ __device__ __forceinline__ int produce_step(char* lds, int wave, int lane, int t
 #endif
     if (!sig_now && !store_now && !dma_now) return prod_next_t(ps, r.U, r.upc, r.lead, r.pcs, t);
     // A signal needs this wave's stores complete: vmcnt(0) (the guide's
-    // hand-off rule); they are >= kSigDelay chunks old, so it waits at most
-    // for the last chunk's stream prefetch.  A store needs the slot's LDS-DMA
-    // landed: it is older than the >= kStoreDelay stream prefetches issued
-    // since (one per chunk), and loads return in order, so vmcnt(kStoreDelay)
-    // is enough and the recent prefetches stay in flight.
+    // hand-off rule); they are >= kSigDelay chunks old, and the chunk loop
+    // skips the stream prefetch ahead of a signal step, so it waits for
+    // nothing recent.  A store needs the slot's LDS-DMA landed: it is older
+    // than the pf_n stream prefetches issued since, and loads return in
+    // order, so vmcnt(pf_n) suffices and those prefetches stay in flight.
     if (drain || sig_now)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (store_now)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPfS ? kStoreDelay : 0) : "memory");
+    else if (store_now) {
+        if (kPfS && ps.pf_n >= 2)
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else if (kPfS && ps.pf_n == 1)
+            asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     const unsigned long long q2 = FST_NOW();
     FST_ADD(lds, 9, q2 - q1);
     if (sig_now) {
-        const int p = ps.s_u / r.upc;
         unsigned* crow = reinterpret_cast<unsigned*>(r.crow);
-        if (ps.s_u + r.An >= min(r.U, (p + 1) * r.upc) && lane == 0)
-            piece_signal(crow + ((size_t)p << (r.pcs + 1)));
+#pragma unroll
+        for (int i = 0; i < kSlotUnits; ++i) {
+            const int u = ps.s_u + i * r.An;
+            const int p = u / r.upc;
+            if (i < ps.s_n && u + r.An >= min(r.U, (p + 1) * r.upc) && lane == 0)
+                piece_signal(crow + ((size_t)p << (r.pcs + 1)));
+        }
         ps.s_u = -1;
     }
     const unsigned long long q3 = FST_NOW();
     FST_ADD(lds, 12, q3 - q2);
     if (store_now) {
-        float* XT = reinterpret_cast<float*>(r.xtrow);
-        unit_store(slot_ptr, XT + (size_t)(r.k_lo + kUnitK * ps.d_u) * r.ldxt, r.ldxt, 0, 0, lane);
+        float* XTr = reinterpret_cast<float*>(r.xtrow);
+#pragma unroll
+        for (int i = 0; i < kSlotUnits; ++i)
+            if (i < ps.d_n) unit_store_u(slot_ptr + i * kUnitBytes, XTr, r.ldxt, r.k_lo, ps.d_u + i * r.An, lane);
         ps.s_u = ps.d_u;
+        ps.s_n = ps.d_n;
         ps.tS = t;
         ps.d_u = -1;
     }
     const unsigned long long q4 = FST_NOW();
     FST_ADD(lds, 10, q4 - q3);
     if (dma_now) {
-        const float* X = reinterpret_cast<const float*>(r.xrow);
-        unit_dma(X + r.k_lo + kUnitK * ps.u_next, r.K, r.mmax + 1, 0, 0,
-                 (unsigned)reinterpret_cast<uintptr_t>(slot_ptr), lane);
+        const float* Xr = reinterpret_cast<const float*>(r.xrow);
         ps.d_u = ps.u_next;
+        int n = 0;
+#pragma unroll
+        for (int i = 0; i < kSlotUnits; ++i)
+            if (ps.u_next < r.U) {
+                unit_dma_u(Xr, r.K, r.mmax, r.k_lo, ps.u_next,
+                           (unsigned)reinterpret_cast<uintptr_t>(slot_ptr) + i * kUnitBytes, lane);
+                ps.u_next += r.An;
+                ++n;
+            }
+        ps.d_n = n;
+        if (ps.u_next >= r.U) ps.u_next = 0x7fffffff;
         ps.tD = t;
-        ps.u_next = ps.u_next + r.An < r.U ? ps.u_next + r.An : 0x7fffffff;
+        ps.pf_n = 0;
     }
     FST_ADD(lds, 11, FST_NOW() - q4);
     if (ps.u_next == 0x7fffffff && ps.d_u < 0 && ps.s_u < 0) return 0x7fffffff;
@@ -1149,12 +1228,10 @@ __device__ __forceinline__ void wait_piece(const char* lds, int p, int lane, boo
     }
     for (int n = 0; !piece_ready(c, tgt); ++n) {
         if (n > kPollLimit) {
-            const float* X = reinterpret_cast<const float*>(r.xrow);
-            float* XT = reinterpret_cast<float*>(r.xtrow);
+            const float* Xr = reinterpret_cast<const float*>(r.xrow);
+            float* XTr = reinterpret_cast<float*>(r.xtrow);
             const int u1 = min(r.U, (p + 1) * r.upc);
-            for (int u = p * r.upc; u < u1; ++u)
-                unit_direct(X + r.k_lo + kUnitK * u, r.K, r.mmax + 1, XT + (size_t)(r.k_lo + kUnitK * u) * r.ldxt,
-                            r.ldxt, 0, 0, lane);
+            for (int u = p * r.upc; u < u1; ++u) unit_direct_u(Xr, r.K, r.mmax, XTr, r.ldxt, r.k_lo, u, lane);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             return;
         }
@@ -1273,12 +1350,13 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
             const int mem_end = members_end(gi0, ncb, P, F->n_items);
             const int An = kProdWaves * (mem_end - gi0);
             const int k_lo = q.c_begin * kTK;
-            const int U = q.c_begin < q.c_end ? (min(q.c_end * kTK, K) - k_lo + kUnitK - 1) / kUnitK : 0;
+            const int U = q.c_begin < q.c_end ? units_of(min(q.c_end * kTK, K) - k_lo) : 0;
             const int pc = F->pc, upc = kUnitsPerChunk * pc;
             const int npieces = (U + upc - 1) / upc;
             // every piece up front when the members cannot keep ahead (an agent
-            // moves a unit every kSigDelay chunks at most; the group needs 12 per chunk)
-            const int lead = (An < kSigDelay * kUnitsPerChunk + 4) ? npieces : min(F->lead, npieces);
+            // moves kSlotUnits units per kSigDelay chunks at most; the group needs
+            // kUnitsPerChunk per chunk, with 20 % margin)
+            const int lead = (An * kSlotUnits * 5 < kSigDelay * kUnitsPerChunk * 6) ? npieces : min(F->lead, npieces);
             const int agent = (!TCSC_FUSED_DIAG_PURE && item < mem_end && prod_wave) ? kProdWaves * (item - gi0) + (wave - kProdWave0) : -1;
             unsigned* const crow0 = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(F->sync) + kFusedSyncHdr) +
                                     2 * ((size_t)q.rt * nch + q.c_begin);
@@ -1297,12 +1375,11 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
                 while (u_next < lead_units) {
                     int nb = 0;
                     for (int u = u_next; u < lead_units && nb < half; u += An, ++nb)
-                        unit_dma(Xr + k_lo + kUnitK * u, K, M - q.m0, 0, 0,
-                                 (unsigned)reinterpret_cast<uintptr_t>(lds) + slot0 + nb * kUnitBytes, lane);
+                        unit_dma_u(Xr, K, M - 1 - q.m0, k_lo, u,
+                                   (unsigned)reinterpret_cast<uintptr_t>(lds) + slot0 + nb * kUnitBytes, lane);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     for (int i = 0; i < nb; ++i, u_next += An)
-                        unit_store(lds + slot0 + i * kUnitBytes, XTr + (size_t)(k_lo + kUnitK * u_next) * ldxt, ldxt, 0,
-                                   0, lane);
+                        unit_store_u(lds + slot0 + i * kUnitBytes, XTr, ldxt, k_lo, u_next, lane);
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0)
@@ -1403,7 +1480,7 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
                 // for the poll wave, the next chunk a producer wave can act at
                 const int pcs = opaque_s(__builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(lds + kFusedStateOff)[12]));
                 int t_evt = 0;
-                ProdState ps{0x7fffffff, -1, -1, 0, 0};
+                ProdState ps{0x7fffffff, -1, 0, -1, 0, 0, 0, 0};
                 // the item record in registers for the loop (a producer step or a
                 // poll then reads no LDS for it: the gather keeps the LDS queue long)
                 const ItemRec rec = load_rec(lds);
@@ -1459,7 +1536,13 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
                         t_evt = produce_step(lds, wave, opaque_v(lane), t, false, ps, rec);
                         if (TCSC_FUSED_PROD_PRIO) __builtin_amdgcn_s_setprio(0);
                     }
-                    pf_issue(cur);
+                    // a producer skips its stream prefetch ahead of a signal step, whose
+                    // vmcnt(0) would otherwise wait for it; it counts the ones it issues
+                    // (a store step's wait leaves that many in flight)
+                    if (!(prod_wave && ps.s_u >= 0 && t + 1 >= ps.tS + kSigDelay)) {
+                        pf_issue(cur);
+                        ps.pf_n = min(ps.pf_n + 1, kStoreDelay);
+                    }
                     dbuf = dbuf == kNBuf - 1 ? 0 : dbuf + 1;
                 }
                 // units still in flight (a group whose gather ends first)

@@ -106,7 +106,8 @@ lib/abl/libtcsc_amd_pfs%.so: $(SRC)/tcsc_kernels.hip $(SRC)/tcsc_api.cpp $(OBJ)/
 #   st  s_memtime stamps (tools/fused_stamps.py)        rr  round-robin item order
 #   late / prio / lp  producer steps after the gather / at raised priority / both
 #   2w  two producer waves, several stages per step (the first layout)   1a  two waves, one stage
-#   3w  three waves, several stages (the default is three waves, one stage per step)
+#   3w  three waves, several stages (the default: 4 k x 256 m units, 3 waves, one stage per step)
+#   small  1 k x 64 m units, 12 waves, one stage per step   sm0  the same, several stages per step
 FDEF_nl := -DTCSC_FUSED_DIAG_NOLOOP=1
 FDEF_pu := -DTCSC_FUSED_DIAG_PURE=1
 FDEF_st := -DTCSC_FUSED_STAMPS=1
@@ -117,6 +118,8 @@ FDEF_lp := -DTCSC_FUSED_PROD_LATE=1 -DTCSC_FUSED_PROD_PRIO=1
 FDEF_2w := -DTCSC_FUSED_PROD_WAVES=2 -DTCSC_FUSED_ONE_ACTION=0
 FDEF_1a := -DTCSC_FUSED_PROD_WAVES=2 -DTCSC_FUSED_ONE_ACTION=1
 FDEF_3w := -DTCSC_FUSED_PROD_WAVES=3 -DTCSC_FUSED_ONE_ACTION=0
+FDEF_small := -DTCSC_FUSED_SMALL=1
+FDEF_sm0 := -DTCSC_FUSED_SMALL=1 -DTCSC_FUSED_ONE_ACTION=0
 lib/abl/libtcsc_amd_f%.so: $(SRC)/tcsc_kernels.hip $(SRC)/tcsc_api.cpp $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o $(HDRS) $(SRC)/gather_asm.inc
 	@mkdir -p lib/abl $(OBJ)/abl
 	$(HIPCC) $(HIPFLAGS) $(FDEF_$*) -c $(SRC)/tcsc_kernels.hip -o $(OBJ)/abl/k_f$*.o
