@@ -848,6 +848,9 @@ __device__ __forceinline__ int xcd_slot(int b, int P) {
 // one XCD's L2 across rounds, as k_stream's tile order keeps them.  The
 // other schedule deals item slot + r*P (a group's items in one round, but
 // split over two XCDs, each reading the row tile into its own L2).
+#ifndef TCSC_FUSED_PF_SKIP  // producers skip the stream prefetch ahead of a signal step
+#define TCSC_FUSED_PF_SKIP TCSC_FUSED_SMALL
+#endif
 #ifndef TCSC_FUSED_ONE_ACTION  // A/B: at most one stage (signal, store or DMA) per producer step
 #define TCSC_FUSED_ONE_ACTION 1
 #endif
@@ -1149,9 +1152,8 @@ __device__ __forceinline__ int produce_step(char* lds, int wave, int lane, int t
 #endif
     if (!sig_now && !store_now && !dma_now) return prod_next_t(ps, r.U, r.upc, r.lead, r.pcs, t);
     // A signal needs this wave's stores complete: vmcnt(0) (the guide's
-    // hand-off rule); they are >= kSigDelay chunks old, and the chunk loop
-    // skips the stream prefetch ahead of a signal step, so it waits for
-    // nothing recent.  A store needs the slot's LDS-DMA landed: it is older
+    // hand-off rule); they are >= kSigDelay chunks old, so it waits at most
+    // for the last chunk's stream prefetch (which TCSC_FUSED_PF_SKIP skips).  A store needs the slot's LDS-DMA landed: it is older
     // than the pf_n stream prefetches issued since, and loads return in
     // order, so vmcnt(pf_n) suffices and those prefetches stay in flight.
     if (drain || sig_now)
@@ -1539,7 +1541,7 @@ __global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const Fuse
                     // a producer skips its stream prefetch ahead of a signal step, whose
                     // vmcnt(0) would otherwise wait for it; it counts the ones it issues
                     // (a store step's wait leaves that many in flight)
-                    if (!(prod_wave && ps.s_u >= 0 && t + 1 >= ps.tS + kSigDelay)) {
+                    if (!(TCSC_FUSED_PF_SKIP && prod_wave && ps.s_u >= 0 && t + 1 >= ps.tS + kSigDelay)) {
                         pf_issue(cur);
                         ps.pf_n = min(ps.pf_n + 1, kStoreDelay);
                     }

@@ -120,6 +120,7 @@ FDEF_1a := -DTCSC_FUSED_PROD_WAVES=2 -DTCSC_FUSED_ONE_ACTION=1
 FDEF_3w := -DTCSC_FUSED_PROD_WAVES=3 -DTCSC_FUSED_ONE_ACTION=0
 FDEF_small := -DTCSC_FUSED_SMALL=1
 FDEF_sm0 := -DTCSC_FUSED_SMALL=1 -DTCSC_FUSED_ONE_ACTION=0
+FDEF_skip := -DTCSC_FUSED_PF_SKIP=1
 lib/abl/libtcsc_amd_f%.so: $(SRC)/tcsc_kernels.hip $(SRC)/tcsc_api.cpp $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o $(HDRS) $(SRC)/gather_asm.inc
 	@mkdir -p lib/abl $(OBJ)/abl
 	$(HIPCC) $(HIPFLAGS) $(FDEF_$*) -c $(SRC)/tcsc_kernels.hip -o $(OBJ)/abl/k_f$*.o
