@@ -126,3 +126,15 @@ lib/abl/libtcsc_amd_f%.so: $(SRC)/tcsc_kernels.hip $(SRC)/tcsc_api.cpp $(OBJ)/tc
 	$(HIPCC) $(HIPFLAGS) $(FDEF_$*) -c $(SRC)/tcsc_kernels.hip -o $(OBJ)/abl/k_f$*.o
 	$(HIPCC) $(HIPFLAGS) $(FDEF_$*) -c $(SRC)/tcsc_api.cpp -o $(OBJ)/abl/a_f$*.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)/abl/k_f$*.o $(OBJ)/abl/a_f$*.o $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o -lpthread -L$(ROCM)/lib -lrocblas -Wl,-rpath,$(ROCM)/lib
+
+# 4-byte entry cost proxy: the generated loop rebuilds the +-1
+# multiplier from a sign bit with 2 SALU per entry (gen_gather_asm.py --sgn 1);
+# results unchanged.  lib/abl/libtcsc_amd_sgn1.so
+$(OBJ)/abl/gather_sgn%.inc: ../tools/gen_gather_asm.py
+	@mkdir -p $(OBJ)/abl
+	python3 ../tools/gen_gather_asm.py --sgn $* -o $@ > /dev/null
+
+lib/abl/libtcsc_amd_sgn%.so: $(OBJ)/abl/gather_sgn%.inc $(SRC)/tcsc_kernels.hip $(SRC)/tcsc_api.cpp $(OBJ)/tcsc_api.o $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o $(HDRS)
+	@mkdir -p lib/abl $(OBJ)/abl
+	$(HIPCC) $(HIPFLAGS) -DTCSC_GATHER_INC='"$(abspath $(OBJ)/abl/gather_sgn$*.inc)"' -c $(SRC)/tcsc_kernels.hip -o $(OBJ)/abl/k_sgn$*.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)/abl/k_sgn$*.o $(OBJ)/tcsc_api.o $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o -lpthread -L$(ROCM)/lib -lrocblas -Wl,-rpath,$(ROCM)/lib
