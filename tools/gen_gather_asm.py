@@ -86,6 +86,8 @@ ABL = 0
 # bit, s_or 1.0's exponent) into a scratch SGPR pair instead of being loaded
 # as the entry's own dword.  The proxy takes the bit from the 8-byte entry's
 # sign dword, so results are unchanged and only the instruction cost moves.
+# SGN = 2: the same 2 SALU a batch ahead (in ISSUE), in place over the sign
+# dword, so no FMA waits on a just-written SGPR.
 SGN = 0
 SGN_BASE = 92  # scratch pairs s[92:93] .. s[98:99], one per batch entry
 
@@ -105,6 +107,11 @@ def issue(g, p, n=None):
     if ABL != 3:
         for i in range(n):
             out.append(f"ds_read_b128 v[{x + 4 * i}:{x + 4 * i + 3}], v{x + 4 * i}")
+    if SGN == 2:
+        # the decode a batch ahead of its FMAs, in place over the entry's sign dword
+        for i in range(n):
+            sg = sreg(g, g.batch * p + i, 0)
+            out += [f"s_and_b32 s{sg}, s{sg}, 0x80000000", f"s_or_b32 s{sg}, s{sg}, 0x3f800000"]
     return out
 
 
@@ -113,7 +120,7 @@ def fma(g, p, wait, n=None):
     n = g.batch if n is None else n
     x = g.xset[p % (g.depth + 1)]
     out = []
-    if SGN and ABL != 4:
+    if SGN == 1 and ABL != 4:
         for i in range(n):
             t = SGN_BASE + 2 * i
             out += [f"s_and_b32 s{t}, s{sreg(g, g.batch * p + i, 0)}, 0x80000000", f"s_or_b32 s{t}, s{t}, 0x3f800000"]
@@ -123,7 +130,7 @@ def fma(g, p, wait, n=None):
     for i in range(n):
         j = g.batch * p + i
         w1, sg = sreg(g, j, 1), sreg(g, j, 0)
-        pair = f"s[{SGN_BASE + 2 * i}:{SGN_BASE + 2 * i + 1}]" if SGN else f"s[{sg}:{sg + 1}]"
+        pair = f"s[{SGN_BASE + 2 * i}:{SGN_BASE + 2 * i + 1}]" if SGN == 1 else f"s[{sg}:{sg + 1}]"
         a = g.acc + 4 * (i % g.cw) if ABL == 1 else g.acc
         if ABL != 1:
             out.append(f"s_set_gpr_idx_on s{w1}, gpr_idx(SRC2,DST)" if i == 0 else f"s_set_gpr_idx_idx s{w1}")
@@ -311,7 +318,7 @@ def write_inc(path, g):
         f.write(f"#define TCSC_GEN_PF {g.pf}\n")
         clob = ['"memory"', '"scc"']
         clob += [f'"v{r}"' for r in range(g.xbase, g.xbase + g.nx)]
-        if SGN:
+        if SGN == 1:
             clob += [f'"s{r}"' for r in range(SGN_BASE, SGN_BASE + 2 * g.batch)]
         f.write("#define TCSC_GATHER_CLOBBERS " + ", ".join(clob) + "\n")
         f.write("#if !defined(TCSC_ABLATION) || TCSC_ABLATION == 0 || TCSC_ABLATION >= 6\n")
@@ -339,7 +346,7 @@ def main():
     ap.add_argument("--tail", type=int, default=1)
     ap.add_argument("--hdr", type=int, default=4, help="chunk-header dwords ahead of the entries")
     ap.add_argument("--pf", type=int, default=0, help="scalar-cache lines prefetched for a stream that will reload")
-    ap.add_argument("--sgn", type=int, default=0, help="1: rebuild the +-1 multiplier from a sign bit (2 SALU per entry)")
+    ap.add_argument("--sgn", type=int, default=0, help="1/2: rebuild the +-1 multiplier from a sign bit (2 SALU per entry; 2: a batch ahead)")
     here = os.path.dirname(os.path.abspath(__file__))
     ap.add_argument("-o", default=os.path.join(here, "..", "sparse-matrix-multiplication-benchmark_amd", "csrc",
                                                "gather_asm.inc"))

@@ -1,17 +1,17 @@
 #!/bin/bash
 # Round-4 A/B: cost of a 4-byte entry stream's sign decode.
-# lib/diag/libtcsc_amd_sgn1.so = tools/ab.mk lib/abl/libtcsc_amd_sgn1.so (2 SALU per entry rebuild the
-# +-1 multiplier from a sign bit; results unchanged) against the default loop, cfg 4, cfg 2 and the
+# lib/diag/libtcsc_amd_sgn<1|2>.so = tools/ab.mk lib/abl/libtcsc_amd_sgn<1|2>.so (2 SALU per entry rebuild
+# the +-1 multiplier from a sign bit, 1: just ahead of the FMA, 2: a batch ahead; results unchanged) against the default loop, cfg 4, cfg 2 and the
 # 8-way block, alternating twice.  The parity tests run on the proxy first.
 set -o pipefail
 Q="--no-cpu-baseline --no-dense-baseline --no-bcsr --no-reference-order --no-other-configs --no-host-api --no-validate"
-L=$PWD/sparse-matrix-multiplication-benchmark_amd/lib/diag/libtcsc_amd_sgn1.so
-TCSC_AMD_LIB=$L timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "not full_size" 2>&1 | tail -1 || exit 1
+D=$PWD/sparse-matrix-multiplication-benchmark_amd/lib/diag
+TCSC_AMD_LIB=$D/libtcsc_amd_sgn2.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "not full_size" 2>&1 | tail -1 || exit 1
 for r in 1 2; do
 for args in "--config 4" "--config 2" "--shard-of 8"; do
-  for v in base sgn; do
+  for v in base sgn1 sgn2; do
     unset TCSC_AMD_LIB
-    [ $v = sgn ] && export TCSC_AMD_LIB=$L
+    [ $v != base ] && export TCSC_AMD_LIB=$D/libtcsc_amd_$v.so
     timeout -k 10 120 python -u bench.py --steps 30 --warmup 5 $args $Q > gpurun_out/c.json 2>gpurun_out/c.err || exit 1
     python3 -c "import json;d=json.load(open('gpurun_out/c.json'));r=d['roofline'];print('$args $v',round(d['ms_per_step'],4),round(r.get('kernel_ms'),4),r.get('path'))"
   done
