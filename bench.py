@@ -288,6 +288,7 @@ def main():
                 "kernel": kernel_name,
                 "path": path,
                 "k_slices": slices,
+                "combine_in_launch": plan.launch_combine(cfg.M) if slices > 1 else False,
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_ms": kernel_s * 1e3,
                 "step_ms_events": step_events_s * 1e3,
@@ -488,7 +489,8 @@ def other_configs(args, tcsc_amd, workloads, dev, sh, timed, skip):
         path = {"mfma": "mfma (bf16 x3 split GEMM: k_split3 + k_gemm3)", "small": "small-M (one wave per column)",
                 "fused": "fused gather (k_fused: X^T written in the same launch)",
                 "gather": "gather (k_transpose + k_stream)"}[lpath] + \
-            (f", K split {lslices} ways + k_reduce4" if lslices > 1 else "")
+            ((f", K split {lslices} ways, combined in the k_stream launch" if plan.launch_combine(c.M) else
+              f", K split {lslices} ways + k_reduce4") if lslices > 1 else "")
         r = {
             "workload": c.describe(), "variant": c.variant, "nnz": nnz, "ms": t * 1e3,
             "g_add_ops_per_s": workloads.add_ops(c.M, nnz, c.N) / t / 1e9,

@@ -114,7 +114,8 @@ int tcsc_gpu_plan_get_info(const tcsc_gpu_plan *plan, tcsc_gpu_plan_info *info);
  * aligned, the plan's reserved workspace and the current environment):
  *   TCSC_PATH_FUSED  k_fused: X^T written by the gather's own workgroups
  *                    (one persistent launch, + k_reduce when K is split)
- *   TCSC_PATH_GATHER k_transpose + k_stream (+ k_reduce)
+ *   TCSC_PATH_GATHER k_transpose + k_stream (+ k_reduce, or the in-launch
+ *                    combine: tcsc_gpu_launch_combine)
  *   TCSC_PATH_MFMA   k_split3 + k_gemm3 (+ k_fixup), near-dense W
  *   TCSC_PATH_SMALL  k_small_m, M <= 16
  * and *slices = the K split of the gather paths (1 = none). */
@@ -125,6 +126,14 @@ enum tcsc_path {
     TCSC_PATH_SMALL = 3
 };
 int tcsc_gpu_launch_info(const tcsc_gpu_plan *plan, int M, int *path, int *slices);
+
+/* For TCSC_PATH_GATHER with a K split: *in_launch = 1 when the split-K slabs
+ * are combined inside the k_stream launch (the grid fits the chip at one
+ * workgroup per CU, >= 3 slices, >= 64 workgroups, N % 4 == 0, the plan's
+ * reserved workspace; TCSC_COMBINE=0/1 overrides the slice and size rule),
+ * 0 when k_reduce runs after it or nothing is split.  Y and bias are assumed
+ * 16-B aligned with ldy = N; otherwise the launch uses k_reduce. */
+int tcsc_gpu_launch_combine(const tcsc_gpu_plan *plan, int M, int *in_launch);
 
 /* Allocate the plan's workspace for launches of up to `max_M` rows: X^T
  * (K x max_M rounded up to 256 floats; the kernel streams X^T rows into LDS)

@@ -634,6 +634,7 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
         g.fsync = p->fsync;
         g.fsync_n = tcsc::fused_sync_pairs(p->fsync_M, p->rows);
         g.num_cus = p->num_cus;
+        g.ccnt = tcsc::combine_words(p->fsync, p->fsync_M, p->rows);
     }
     // Bias first for tcsc_sgemm_basic (tcsc.c:74-96), last otherwise
     // (tcsc.c:149-161; the optimized family adds per-sign partial sums to
@@ -879,6 +880,27 @@ int tcsc_gpu_launch_info(const tcsc_gpu_plan* p, int M, int* path, int* slices) 
         *slices = M > (1 << 22) ? 1
                                 : tcsc::choose_slices(rows, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups,
                                                       p->ws_bytes > xtb ? p->ws_bytes - xtb : 0, slices_override());
+    return TCSC_OK;
+}
+
+int tcsc_gpu_launch_combine(const tcsc_gpu_plan* p, int M, int* in_launch) {
+    if (!p || M < 0 || !in_launch) {
+        set_error("tcsc_gpu_launch_combine: bad arguments");
+        return TCSC_E_ARG;
+    }
+    *in_launch = 0;
+    int path = 0, slices = 1;
+    const int rc = tcsc_gpu_launch_info(p, M, &path, &slices);
+    if (rc != TCSC_OK) return rc;
+    if (path != TCSC_PATH_GATHER || slices <= 1) return TCSC_OK;
+    const int rows = std::min(M, 1 << 22);
+    const int s = tcsc::normalized_slices(p->rows, slices);
+    const long long cb = (p->n_groups + tcsc::kWaves - 1) / tcsc::kWaves, rt = (rows + tcsc::kTM - 1) / tcsc::kTM;
+    const bool words = p->fsync && rows <= p->fsync_M;
+    *in_launch = tcsc::combine_applies(s, cb * rt * s, cb * rt, (long long)rows * p->cols, words ? p->num_cus : 0,
+                                       words, p->cols % 4 == 0)
+                     ? 1
+                     : 0;
     return TCSC_OK;
 }
 

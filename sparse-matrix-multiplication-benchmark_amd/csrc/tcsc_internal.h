@@ -228,7 +228,19 @@ inline int fused_sync_pairs(int M, int K) {
     const int nrt = (M + kTM - 1) / kTM, nch = (K + kTK - 1) / kTK;
     return nrt * (nch > 0 ? nch : 1);
 }
-inline size_t fused_sync_bytes(int M, int K) { return kFusedSyncHdr + (size_t)fused_sync_pairs(M, K) * 8; }
+// + the in-launch split-K combine's tile words (k_stream OUT 2, after the
+// piece counters): per tile {arrivals, done, claims[Z]}, reset by the tile's
+// last workgroup, so every launch finds them zero
+constexpr int kCombineTiles = 256;
+constexpr int kCombineWords = 32;  // per tile: 2 + Z (Z <= 16) used
+inline size_t fused_sync_bytes(int M, int K) {
+    return kFusedSyncHdr + (size_t)fused_sync_pairs(M, K) * 8 + (size_t)kCombineTiles * kCombineWords * 4;
+}
+inline unsigned* combine_words(unsigned* sync, int M, int K) {
+    return sync ? reinterpret_cast<unsigned*>(reinterpret_cast<char*>(sync) + kFusedSyncHdr +
+                                              (size_t)fused_sync_pairs(M, K) * 8)
+                : nullptr;
+}
 
 struct FusedArgs {
     const float* X = nullptr;       // M x K row-major
@@ -281,6 +293,7 @@ struct GemmArgs {
     unsigned* fsync = nullptr;
     int fsync_n = 0;           // counter pairs in fsync (fused_sync_pairs of the size it was made for)
     int num_cus = 0;           // persistent grid size (workgroups, one per CU)
+    unsigned* ccnt = nullptr;  // the split-K combine's tile words (combine_words of fsync)
 };
 
 // Plan building
@@ -289,6 +302,10 @@ hipError_t plan_counts(const PlanDev& in, PlanOut& out, hipStream_t st);    // -
 hipError_t plan_fill(const PlanDev& in, PlanOut& out, hipStream_t st);      // -> sptr, ent
 // Launch
 int choose_slices(int M, int ncols, int K, long long nnz, int n_groups, size_t ws_bytes, int force);
+// the split-K combine of a gather launch runs inside k_stream (combine_tile)
+bool combine_applies(int slices, long long wgs, long long tiles, long long slab_floats, int num_cus, bool have_words,
+                     bool vec);
+int normalized_slices(int K, int slices);  // the K split launch_gemm actually runs
 // stream prefetch of a plan of n_entries entries over n_groups x n_chunks
 // streams: *dist bytes ahead, *lines 128-B lines (TCSC_PF_DIST / TCSC_PF_LINES override)
 void pf_stream_params(long long n_entries, int n_groups, int n_chunks, int* dist, int* lines);

@@ -476,7 +476,122 @@ __device__ __forceinline__ unsigned long long stamp() {
 }
 #endif
 
+// In-launch split-K combine (k_stream OUT 2; DESIGN.md §4 k_reduce).  The
+// Z workgroups of a tile (its K slices) each write their slab with sc1
+// (write-through) stores, drain them (vmcnt(0) in every wave, barrier) and
+// add 1 to the tile's arrival word (lane 0, agent scope).  Each then owns
+// row band z of the tile: it polls the arrival word (sc1 loads, s_sleep)
+// until all Z have arrived, claims its band (compare-and-swap 0 -> 1) and
+// reduces it from all Z slabs with sc1 loads -- the same adds in the same
+// order as k_reduce4, so the same bits.  The workgroup whose add came last
+// knows the slabs are complete without polling; after its own band it
+// claims and reduces any band still unclaimed, so a workgroup whose poll
+// gives up (kCombineSpin polls: a slice that is not resident) leaves no band
+// undone, and no band is reduced twice.  The last workgroup to finish
+// (the done word) zeroes the tile's words for the next launch.  The host
+// takes this path only when the grid fits the chip at one workgroup per CU
+// (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility",
+// the counter hand-off row: sc1 stores, vmcnt(0), barrier, one agent add,
+// sc1 poll or the add's return value, barrier, sc1 loads).
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4c_t __attribute__((ext_vector_type(4)));
+constexpr int kSc1 = 16;  // buffer cache-policy bits: sc1
+constexpr int kCombineSpin = 1 << 20;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slabs_rsrc(float* ws, int Z, int M, int ncols) {
+    const long long bytes = (long long)Z * M * ncols * 4;
+    return __builtin_amdgcn_make_buffer_rsrc(ws, 0, (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL), 0x00020000);
+}
+
+template <bool BIAS_FIRST, bool PRELU>
+__device__ __forceinline__ void combine_tile(float* ws, int M, int ncols, const float* __restrict__ Bias,
+                                             float* __restrict__ Y, int ldy, float a, unsigned* ccnt, const Tile t,
+                                             char* lds) {
+    const int Z = (int)gridDim.z;
+    unsigned* w = ccnt + (size_t)(t.rt * (int)gridDim.x + t.cb) * kCombineWords;  // {arrivals, done, claims[Z]}
+    int* flag = reinterpret_cast<int*>(lds);  // the epilogue's staging is done (barrier below)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores have left
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int st = old + 1 == (unsigned)Z ? 2 : 0;  // 2: the last arrival, 1: saw all arrive, 0: gave up
+        for (int n = 0; st == 0 && n < kCombineSpin; ++n) {
+            if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)Z)
+                st = 1;
+            else
+                __builtin_amdgcn_s_sleep(4);
+        }
+        flag[0] = st;
+    }
+    __syncthreads();
+    const int st = __builtin_amdgcn_readfirstlane(flag[0]);
+    const __amdgpu_buffer_rsrc_t rs = slabs_rsrc(ws, Z, M, ncols);
+    const int m0 = t.rt * kTM, c0 = t.cb * kWgCols;
+    const size_t slab = (size_t)M * ncols;
+    auto claim = [&](int q) {
+        __syncthreads();  // everyone has read the previous flag
+        if (threadIdx.x == 0) {
+            unsigned expect = 0u;
+            flag[1] = __hip_atomic_compare_exchange_strong(w + 2 + q, &expect, 1u, __ATOMIC_RELAXED,
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          ? 1
+                          : 0;
+        }
+        __syncthreads();
+        return __builtin_amdgcn_readfirstlane(flag[1]) != 0;
+    };
+    auto reduce_band = [&](int q) {
+        constexpr int nq = kWgCols / 4;
+        const int r0 = kTM * q / Z, r1 = kTM * (q + 1) / Z;
+        for (int i = threadIdx.x; i < (r1 - r0) * nq; i += kWaves * 64) {
+            const int row = m0 + r0 + i / nq, col = c0 + 4 * (i % nq);
+            if (row >= M || col >= ncols) continue;
+            const int off = (int)((size_t)row * ncols + col) * 4;
+            f32x4c_t p[16];
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+                if (s < Z)
+                    p[s] = __builtin_bit_cast(
+                        f32x4c_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off, (int)(s * slab * 4), kSc1));
+            const float4 b = *reinterpret_cast<const float4*>(Bias + col);
+            float4 v = BIAS_FIRST ? b : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+                if (s < Z) {
+                    v.x += p[s].x;
+                    v.y += p[s].y;
+                    v.z += p[s].z;
+                    v.w += p[s].w;
+                }
+            if (!BIAS_FIRST) {
+                v.x += b.x;
+                v.y += b.y;
+                v.z += b.z;
+                v.w += b.w;
+            }
+            if (PRELU) {
+                v.x = (v.x < 0.0f) ? a * v.x : v.x;
+                v.y = (v.y < 0.0f) ? a * v.y : v.y;
+                v.z = (v.z < 0.0f) ? a * v.z : v.z;
+                v.w = (v.w < 0.0f) ? a * v.w : v.w;
+            }
+            typedef float nt4 __attribute__((ext_vector_type(4)));
+            nt4 o = {v.x, v.y, v.z, v.w};
+            __builtin_nontemporal_store(o, reinterpret_cast<nt4*>(Y + (size_t)row * ldy + col));
+        }
+    };
+    if (st != 0 && claim(t.z)) reduce_band(t.z);
+    if (st == 2)
+        for (int q = 0; q < Z; ++q)
+            if (q != t.z && claim(q)) reduce_band(q);
+    __syncthreads();
+    if (threadIdx.x == 0 && __hip_atomic_fetch_add(w + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 ==
+                                (unsigned)Z) {
+        for (int i = 0; i < 2 + Z; ++i) __hip_atomic_store(w + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // OUT: 0 = final Y (bias + activation), 1 = partial slab ws[slice][M][ncols]
+// (k_reduce combines), 2 = the slab, then the in-launch combine (combine_tile)
 // ORDER (the summation order, DESIGN.md "Numerics"):
 //   0  one plan, each column's +1 and -1 entries merged by ascending k;
 //   1  the reference's order for tcsc_sgemm_basic / _prelu_basic
@@ -495,7 +610,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
          const int* __restrict__ sptr, long long n_entries, const int2* __restrict__ ent2,
          const int* __restrict__ sptr2, long long n_entries2, int G, int ncols, int nch, int chunks_per_slice,
          const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a, float* __restrict__ ws, int pf_dist,
-         int pf_lines) {
+         int pf_lines, unsigned* __restrict__ ccnt) {
     static_assert(ORDER == 0 || OUT == 0, "the reference orders do not split K");
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const int lane = threadIdx.x & 63;
@@ -665,6 +780,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         const int col_end = min(col0 + wave_cols(wave), ncols);  // this wave's columns: [col0, col_end)
         const bool vec_ok = OUT == 0 ? ((ldy & 3) == 0 && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0))
                                      : ((ncols & 3) == 0 && ((reinterpret_cast<uintptr_t>(ws) & 15) == 0));
+        const __amdgpu_buffer_rsrc_t slab_rs = slabs_rsrc(ws, (int)gridDim.z, M, ncols);
         constexpr bool kAddBias = OUT == 0 && (HOW == 1 || (HOW == 0 && !BIAS_FIRST));
         constexpr bool kPrelu = PRELU && HOW != 1;
 #pragma unroll
@@ -726,7 +842,27 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                         } else {
                             dst = ws + ((size_t)t.z * M + row) * ncols + col;
                         }
-                        if (vec_ok && col + 3 < col_end) {
+                        if constexpr (OUT == 2) {
+                            // write-through (sc1) slab stores: the tile's other
+                            // workgroups read them with sc1 loads (combine_tile)
+                            const int off = (int)(((size_t)t.z * M + row) * ncols + col) * 4;
+                            if (vec_ok && col + 3 < col_end) {
+                                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), slab_rs, off, 0,
+                                                                       kSc1);
+                            } else {
+                                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v.x), slab_rs, off, 0,
+                                                                      kSc1);
+                                if (col + 1 < col_end)
+                                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v.y), slab_rs,
+                                                                          off + 4, 0, kSc1);
+                                if (col + 2 < col_end)
+                                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v.z), slab_rs,
+                                                                          off + 8, 0, kSc1);
+                                if (col + 3 < col_end)
+                                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v.w), slab_rs,
+                                                                          off + 12, 0, kSc1);
+                            }
+                        } else if (vec_ok && col + 3 < col_end) {
                             if (OUT == 0 && HOW != 1) {  // Y is never re-read here: keep it out of L2's way
                                 typedef float nt4 __attribute__((ext_vector_type(4)));
                                 nt4 w = {v.x, v.y, v.z, v.w};
@@ -750,6 +886,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     run_chain(ent, sptr, n_entries);
     if constexpr (ORDER == 0) {
         epilogue(std::integral_constant<int, 0>{});
+        if constexpr (OUT == 2) combine_tile<BIAS_FIRST, PRELU>(ws, M, ncols, Bias, Y, ldy, a, ccnt, t, lds);
     } else if constexpr (ORDER == 1) {
         __syncthreads();  // every wave is done with the ring before the -1 chain refills it
         run_chain(ent2, sptr2, n_entries2);
@@ -1692,6 +1829,9 @@ __global__ void k_reduce(const float* __restrict__ ws, int slices, int M, int nc
 // flight before the adds); same order per element, so the same bits.  Needs
 // ncols % 4 == 0, ldy % 4 == 0 and 16-B aligned ws, Y.
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+#ifndef TCSC_REDUCE_NT
+#define TCSC_REDUCE_NT 1  // slab loads nontemporal (A/B: tools/ab.mk lib/abl/libtcsc_amd_rnt0.so)
+#endif
 template <bool BIAS_FIRST, bool PRELU>
 __global__ void k_reduce4(const f32x4_t* __restrict__ ws, int slices, int M, int ncols,
                           const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a) {
@@ -1703,7 +1843,8 @@ __global__ void k_reduce4(const f32x4_t* __restrict__ ws, int slices, int M, int
         f32x4_t p[16];
 #pragma unroll
         for (int s = 0; s < 16; ++s)
-            if (s < slices) p[s] = __builtin_nontemporal_load(ws + (size_t)s * total + i);
+            if (s < slices) p[s] = TCSC_REDUCE_NT ? __builtin_nontemporal_load(ws + (size_t)s * total + i)
+                                                  : ws[(size_t)s * total + i];
         const float4 b = *reinterpret_cast<const float4*>(Bias + col);
         float4 v = BIAS_FIRST ? b : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -2001,6 +2142,29 @@ void pf_stream_params(long long n_entries, int n_groups, int n_chunks, int* dist
     *lines = l;
 }
 
+// Split-K slabs combined inside the k_stream launch (combine_tile) where the
+// grid is resident at once, or by k_reduce4 after it.  TCSC_COMBINE unset:
+// in-launch from 3 slices and 64 workgroups on (measured: cfg 2/3 at 4
+// slices 79 -> 74 us; the 8-way cfg 4 block at 2 slices 0.186 -> 0.192 ms, a
+// tile's two slices wait on each other longer than the reduce launch takes;
+// cfg 1's 6 workgroups 23 -> 27 us, the hand-off's atomics in series cost
+// more than a launch); 1: wherever it applies; 0: never.
+bool combine_applies(int slices, long long wgs, long long tiles, long long slab_floats, int num_cus, bool have_words,
+                     bool vec) {
+    if (slices < 2 || slices > 16 || !vec || !have_words || num_cus <= 0 || wgs > num_cus || tiles > kCombineTiles ||
+        slab_floats * slices * 4 >= 0x7fffffffLL)
+        return false;
+    const int c = env_int("TCSC_COMBINE", -1);
+    return c < 0 ? (slices >= 3 && wgs >= 64) : c != 0;
+}
+
+int normalized_slices(int K, int slices) {
+    const int nch = (K + kTK - 1) / kTK;
+    if (nch <= 0) return 1;
+    const int cps = (nch + slices - 1) / slices;
+    return (nch + cps - 1) / cps;
+}
+
 template <bool BF, bool PR>
 static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
     const int nch = (g.K + kTK - 1) / kTK;
@@ -2015,30 +2179,39 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
     if (g.order == 1) {
         hipLaunchKernelGGL((k_stream<BF, PR, 0, 1>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
                            g.n_entries, g.ent2, g.sptr2, g.n_entries2, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy,
-                           g.a, g.ws, pfd, pfl);
+                           g.a, g.ws, pfd, pfl, nullptr);
         return hipGetLastError();
     }
     if (g.order == 2) {
         hipLaunchKernelGGL((k_stream<false, PR, 0, 2>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
                            g.n_entries, g.ent2, g.sptr2, g.n_entries2, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy,
-                           g.a, g.ws, pfd, pfl);
+                           g.a, g.ws, pfd, pfl, nullptr);
         return hipGetLastError();
     }
     if (slices == 1) {
         hipLaunchKernelGGL((k_stream<BF, PR, 0, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
                            g.n_entries, g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy,
-                           g.a, g.ws, pfd, pfl);
+                           g.a, g.ws, pfd, pfl, nullptr);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((k_stream<BF, PR, 1, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr, g.n_entries,
-                       g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws, pfd,
-                       pfl);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
     const long long total = (long long)g.M * g.ncols;
     const bool vec = slices <= 16 && g.ncols % 4 == 0 && g.ldy % 4 == 0 &&
                      ((reinterpret_cast<uintptr_t>(g.Y) | reinterpret_cast<uintptr_t>(g.ws) |
                        reinterpret_cast<uintptr_t>(g.B)) & 15) == 0;
+    // the in-launch combine (combine_tile): every workgroup of the grid
+    // resident at once (one per CU), so a tile's slices can wait for each other
+    if (combine_applies(slices, (long long)grid.x * grid.y * grid.z, (long long)grid.x * grid.y, total, g.num_cus,
+                        g.ccnt != nullptr, vec)) {
+        hipLaunchKernelGGL((k_stream<BF, PR, 2, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
+                           g.n_entries, g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a,
+                           g.ws, pfd, pfl, g.ccnt);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL((k_stream<BF, PR, 1, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr, g.n_entries,
+                       g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws, pfd,
+                       pfl, nullptr);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
     if (vec)
         hipLaunchKernelGGL((k_reduce4<BF, PR>), dim3(grid_for(total / 4, 256)), dim3(256), 0, st,
                            reinterpret_cast<const f32x4_t*>(g.ws), slices, g.M, g.ncols, g.B, g.Y, g.ldy, g.a);

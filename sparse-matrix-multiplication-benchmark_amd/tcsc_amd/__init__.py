@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_gpu_plan_reserve", "tcsc_gpu_plan_destroy", "tcsc_gpu_sgemm", "tcsc_gpu_prepare_x",
     "tcsc_gpu_sgemm_prepared", "tcsc_gpu_from_dense", "tcsc_gpu_dense_sgemm", "tcsc_gpu_last_error",
     "tcsc_gpu_cache_clear", "tcsc_gpu_num_shards", "tcsc_gpu_set_num_shards", "tcsc_gpu_set_order",
-    "tcsc_gpu_get_order", "tcsc_gpu_launch_info",
+    "tcsc_gpu_get_order", "tcsc_gpu_launch_info", "tcsc_gpu_launch_combine",
     # include/sparse/bcsr.h
     "bcsr_from_dense", "bcsr_sgemm_basic", "bcsr_sgemm_prelu_basic", "bcsr_sgemm_avx", "bcsr_sgemm_prelu_avx",
     "bcsr_sgemm_avx2", "bcsr_free",
@@ -129,6 +129,7 @@ def lib():
     L.tcsc_gpu_plan_create_device.argtypes = [i, i, vp, vp, vp, vp, i, i, i, vp, C.POINTER(vp)]
     L.tcsc_gpu_plan_get_info.argtypes = [vp, C.POINTER(plan_info_t)]
     L.tcsc_gpu_launch_info.argtypes = [vp, i, C.POINTER(i), C.POINTER(i)]
+    L.tcsc_gpu_launch_combine.argtypes = [vp, i, C.POINTER(i)]
     L.tcsc_gpu_plan_reserve.argtypes = [vp, i]
     L.tcsc_gpu_plan_destroy.argtypes = [vp]
     L.tcsc_gpu_plan_destroy.restype = None
@@ -453,6 +454,13 @@ class Plan:
         _check(lib().tcsc_gpu_launch_info(self.handle, int(M), C.byref(path), C.byref(slices)),
                "tcsc_gpu_launch_info")
         return ("gather", "fused", "mfma", "small")[path.value], slices.value
+
+    def launch_combine(self, M: int) -> bool:
+        """True when a gather launch of M rows combines its split-K slabs inside
+        k_stream instead of a k_reduce launch (tcsc_gpu_launch_combine)."""
+        v = C.c_int()
+        _check(lib().tcsc_gpu_launch_combine(self.handle, int(M), C.byref(v)), "tcsc_gpu_launch_combine")
+        return bool(v.value)
 
     def reserve(self, max_M: int) -> None:
         """Allocate the workspace (X^T + split-K slabs) for launches of up to max_M rows."""

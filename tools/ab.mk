@@ -138,3 +138,9 @@ lib/abl/libtcsc_amd_sgn%.so: $(OBJ)/abl/gather_sgn%.inc $(SRC)/tcsc_kernels.hip 
 	@mkdir -p lib/abl $(OBJ)/abl
 	$(HIPCC) $(HIPFLAGS) -DTCSC_GATHER_INC='"$(abspath $(OBJ)/abl/gather_sgn$*.inc)"' -c $(SRC)/tcsc_kernels.hip -o $(OBJ)/abl/k_sgn$*.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)/abl/k_sgn$*.o $(OBJ)/tcsc_api.o $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o -lpthread -L$(ROCM)/lib -lrocblas -Wl,-rpath,$(ROCM)/lib
+
+# split-K combine slab loads: nontemporal (default) or cached (rnt0)
+lib/abl/libtcsc_amd_rnt%.so: $(SRC)/tcsc_kernels.hip $(OBJ)/tcsc_api.o $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o $(HDRS) $(SRC)/gather_asm.inc
+	@mkdir -p lib/abl $(OBJ)/abl
+	$(HIPCC) $(HIPFLAGS) -DTCSC_REDUCE_NT=$* -c $(SRC)/tcsc_kernels.hip -o $(OBJ)/abl/k_rnt$*.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)/abl/k_rnt$*.o $(OBJ)/tcsc_api.o $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o -lpthread -L$(ROCM)/lib -lrocblas -Wl,-rpath,$(ROCM)/lib
