@@ -209,18 +209,18 @@ def main():
         return a_ev.elapsed_time(b_ev) / 1e3 / n
 
     nsplit = max(args.steps, 5)
-    # the step's own kernels: k_fused (the persistent gather that writes its own
-    # X^T, + k_reduce when K is split) -- or, where the fused path does not
-    # apply, k_transpose + k_stream -- timed with HIP events on the launch stream
+    # the step's kernels (k_transpose, then k_stream, + k_reduce4 when K is
+    # split and not combined in the launch), timed with HIP events on the
+    # launch stream: the whole step, then the X^T staging and the gather apart
     path, slices = plan.launch_info(cfg.M)
     step_kernels_s = timed(step, nsplit)
-    # the two-kernel path of the same step, split (diagnostic, not `value`)
     transpose_s = timed(lambda: plan.prepare_x(X, cfg.M, sh), nsplit)
     plan.prepare_x(X, cfg.M, sh)
     gather_s = timed(lambda: plan.sgemm_prepared(B, Y, cfg.M, ncols, variant, 0.2, sh), nsplit)
-    kernel_s = step_kernels_s if path == "fused" else gather_s
-    kernel_name = ("k_fused" + (f" + k_reduce4 ({slices} K slices)" if slices > 1 else "")) if path == "fused" else \
-        "k_stream"
+    kernel_s = gather_s
+    combine = plan.launch_combine(cfg.M) if slices > 1 else False
+    kernel_name = "k_stream" + ((" (+ in-launch combine)" if combine else " + k_reduce4") + f", {slices} K slices"
+                                if slices > 1 else "")
 
     alt = None
     if distributed and args.scaling == "strong" and not args.no_alt_shard and args.shard_of <= 1:
@@ -288,12 +288,17 @@ def main():
                 "kernel": kernel_name,
                 "path": path,
                 "k_slices": slices,
-                "combine_in_launch": plan.launch_combine(cfg.M) if slices > 1 else False,
+                "combine_in_launch": combine,
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_ms": kernel_s * 1e3,
                 "step_ms_events": step_events_s * 1e3,
-                "two_kernel_path": {"k_transpose_ms": transpose_s * 1e3, "k_stream_ms": gather_s * 1e3,
-                                    "note": "TCSC_FUSED=0 path of the same step, split (diagnostic)"},
+                # the same algorithmic bytes over the whole step (k_transpose
+                # included): the HBM fraction that matches `value`
+                "step_achieved": algo_bytes / (elapsed_max / args.steps) / 1e9,
+                "step_frac": algo_bytes / (elapsed_max / args.steps) / 1e9 / HBM_PEAK_GBS,
+                "step_parts_ms": {"k_transpose": transpose_s * 1e3, "gather": gather_s * 1e3,
+                                  "step_kernels": step_kernels_s * 1e3,
+                                  "note": "HIP events on the launch stream, each averaged over the same launches"},
                 "lds_gather_frac": (cfg.M * nnz / kernel_s) / LDS_GATHER_PEAK,
                 "valu_add_frac": (adds_per_launch / kernel_s) / VALU_ADD_PEAK,
             },
@@ -487,7 +492,6 @@ def other_configs(args, tcsc_amd, workloads, dev, sh, timed, skip):
         lpath, lslices = plan.launch_info(c.M)
         mfma = lpath == "mfma"
         path = {"mfma": "mfma (bf16 x3 split GEMM: k_split3 + k_gemm3)", "small": "small-M (one wave per column)",
-                "fused": "fused gather (k_fused: X^T written in the same launch)",
                 "gather": "gather (k_transpose + k_stream)"}[lpath] + \
             ((f", K split {lslices} ways, combined in the k_stream launch" if plan.launch_combine(c.M) else
               f", K split {lslices} ways + k_reduce4") if lslices > 1 else "")
@@ -498,10 +502,15 @@ def other_configs(args, tcsc_amd, workloads, dev, sh, timed, skip):
             "path": path,
         }
         if mfma:
-            ldk = (3 * c.K + 63) // 64 * 64  # the split GEMM's depth (tcsc_internal.h mfma_ldk)
+            # the split GEMM's depth: 3 parts of 32-k blocks, rounded up to the
+            # 64-deep k step (tcsc_internal.h mfma_ldk)
+            ldk = (3 * 32 * ((c.K + 31) // 32) + 63) // 64 * 64
             flops = 2.0 * c.M * c.N * ldk
             r["mfma_flops_per_step"] = flops
             r["mfma_frac"] = flops / t / MFMA_BF16_PEAK
+            # the north star's add/sub-only contract on the same W (tcsc.c:86-93): the
+            # gather path timed beside the MFMA one (a plan made with TCSC_PATH=gather)
+            r["gather_path"] = gather_leg(tcsc_amd, workloads, c, inp, csp, csn, rip, rin, nnz, dev, sh, timed)
         else:
             r["lds_gather_frac"] = (c.M * nnz / t) / LDS_GATHER_PEAK
         if not args.no_cpu_baseline:
@@ -514,6 +523,40 @@ def other_configs(args, tcsc_amd, workloads, dev, sh, timed, skip):
         del inp, csp, csn, rip, rin, Yc
     torch.cuda.empty_cache()
     return res
+
+
+def gather_leg(tcsc_amd, workloads, c, inp, csp, csn, rip, rin, nnz, dev, sh, timed):
+    """The add/sub-only gather path (k_transpose + k_stream) on a config the
+    cost model sends to the MFMA path: the same W in a plan built with
+    TCSC_PATH=gather, the same protocol (10 warm-up + 30 timed launches)."""
+    import torch
+
+    old = os.environ.get("TCSC_PATH")
+    os.environ["TCSC_PATH"] = "gather"
+    try:
+        gp = tcsc_amd.Plan.from_device(c.K, c.N, csp, csn, rip, rin, 0, c.N, dev.index or 0, sh)
+    finally:
+        if old is None:
+            del os.environ["TCSC_PATH"]
+        else:
+            os.environ["TCSC_PATH"] = old
+    gp.reserve(c.M)
+    Yg = torch.empty((c.M, c.N), device=dev)
+
+    def one():
+        gp.sgemm(inp["X"], inp["B"], Yg, c.M, c.N, c.variant, 0.2, sh)
+
+    for _ in range(10):
+        one()
+    t = timed(one, 30)
+    lpath, lslices = gp.launch_info(c.M)
+    gp.destroy()
+    del Yg
+    return {"path": f"{lpath} (k_transpose + k_stream{f', K split {lslices} ways' if lslices > 1 else ''}), "
+                    "add/sub only, no MFMA", "ms": t * 1e3,
+            "g_add_ops_per_s": workloads.add_ops(c.M, nnz, c.N) / t / 1e9,
+            "hbm_frac": workloads.algorithmic_bytes(c.M, c.K, c.N, nnz) / t / (HBM_PEAK_GBS * 1e9),
+            "lds_gather_frac": (c.M * nnz / t) / LDS_GATHER_PEAK}
 
 
 def validate_against_dense(tcsc_amd, cfg, ncols, variant, X, Wd, B, Y, step, sh):

@@ -112,8 +112,6 @@ int tcsc_gpu_plan_get_info(const tcsc_gpu_plan *plan, tcsc_gpu_plan_info *info);
 
 /* Which kernels a tcsc_gpu_sgemm of M rows on this plan runs (with X 16-B
  * aligned, the plan's reserved workspace and the current environment):
- *   TCSC_PATH_FUSED  k_fused: X^T written by the gather's own workgroups
- *                    (one persistent launch, + k_reduce when K is split)
  *   TCSC_PATH_GATHER k_transpose + k_stream (+ k_reduce, or the in-launch
  *                    combine: tcsc_gpu_launch_combine)
  *   TCSC_PATH_MFMA   k_split3 + k_gemm3 (+ k_fixup), near-dense W
@@ -121,7 +119,7 @@ int tcsc_gpu_plan_get_info(const tcsc_gpu_plan *plan, tcsc_gpu_plan_info *info);
  * and *slices = the K split of the gather paths (1 = none). */
 enum tcsc_path {
     TCSC_PATH_GATHER = 0,
-    TCSC_PATH_FUSED = 1,
+    TCSC_PATH_FUSED = 1, /* retired (round 5): the persistent k_fused left the library; never returned */
     TCSC_PATH_MFMA = 2,
     TCSC_PATH_SMALL = 3
 };

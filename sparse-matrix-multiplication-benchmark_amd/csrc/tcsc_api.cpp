@@ -68,14 +68,16 @@ struct tcsc_gpu_plan {
     size_t mfma_bytes = 0;
     // the column range's rebased CSC (fast-order plans): the small-M path
     // walks it, the MFMA path's fixup recomputes flagged rows from it
-    int *ccp = nullptr, *ccn = nullptr, *crp = nullptr, *crn = nullptr;
+    // (crm: each column's +1 / -1 rows merged in ascending k, -1 tagged in bit 31)
+    int *ccp = nullptr, *ccn = nullptr, *crm = nullptr;
     size_t csc_bytes = 0;
     int mfma_min_M = 0;
-    // the fused persistent gather's synchronisation block (tcsc::fused_sync_bytes
-    // for up to fsync_M rows; zeroed once, then each launch zeroes the
-    // counter set the next launch uses) and the persistent grid size
-    unsigned* fsync = nullptr;
-    int fsync_M = 0;
+    // the in-launch split-K combine's tile words (tcsc::kCombineBytes, zeroed
+    // when allocated; every completed launch leaves them at zero) and the CU
+    // count its residency rule needs.  A launch that fails to enqueue marks
+    // them dirty and the next launch re-zeroes them first.
+    unsigned* csync = nullptr;
+    mutable bool csync_dirty = false;
     int num_cus = 0;
 };
 
@@ -271,9 +273,9 @@ void free_mfma(tcsc_gpu_plan* p) {
 }
 
 void free_csc(tcsc_gpu_plan* p) {
-    for (void* q : {(void*)p->ccp, (void*)p->ccn, (void*)p->crp, (void*)p->crn})
+    for (void* q : {(void*)p->ccp, (void*)p->ccn, (void*)p->crm})
         if (q) (void)hipFree(q);
-    p->ccp = p->ccn = p->crp = p->crn = nullptr;
+    p->ccp = p->ccn = p->crm = nullptr;
     p->csc_bytes = 0;
 }
 
@@ -283,17 +285,20 @@ void free_csc(tcsc_gpu_plan* p) {
 int build_csc(tcsc_gpu_plan* p, const int* csp, const int* csn, const int* rip, const int* rin, int col_begin,
               hipStream_t st) {
     if (p->cols == 0) return TCSC_OK;
+    DevBuf trp, trn;  // the rebased per-sign lists, merged into crm
     if (hipMalloc(&p->ccp, (size_t)(p->cols + 1) * sizeof(int)) != hipSuccess ||
         hipMalloc(&p->ccn, (size_t)(p->cols + 1) * sizeof(int)) != hipSuccess ||
-        hipMalloc(&p->crp, (size_t)(p->n_pos > 0 ? p->n_pos : 1) * sizeof(int)) != hipSuccess ||
-        hipMalloc(&p->crn, (size_t)(p->n_neg > 0 ? p->n_neg : 1) * sizeof(int)) != hipSuccess) {
+        hipMalloc(&p->crm, (size_t)(p->n_pos + p->n_neg > 0 ? p->n_pos + p->n_neg : 1) * sizeof(int)) != hipSuccess ||
+        trp.alloc((size_t)(p->n_pos > 0 ? p->n_pos : 1) * sizeof(int)) != hipSuccess ||
+        trn.alloc((size_t)(p->n_neg > 0 ? p->n_neg : 1) * sizeof(int)) != hipSuccess) {
         (void)hipGetLastError();
         free_csc(p);
         return TCSC_OK;
     }
     p->csc_bytes = 2 * (size_t)(p->cols + 1) * sizeof(int) + (size_t)(p->n_pos + p->n_neg) * sizeof(int);
-    HIP_TRY(tcsc::csc_copy(csp, csn, rip, rin, col_begin, p->cols, p->n_pos, p->n_neg, p->ccp, p->ccn, p->crp,
-                           p->crn, st));
+    HIP_TRY(tcsc::csc_copy(csp, csn, rip, rin, col_begin, p->cols, p->n_pos, p->n_neg, p->ccp, p->ccn,
+                           trp.as<int>(), trn.as<int>(), p->crm, st));
+    HIP_TRY(hipStreamSynchronize(st));  // the temporaries are freed on return
     return TCSC_OK;
 }
 
@@ -393,6 +398,14 @@ int build_plan_ordered(int rows, int col_begin, int ncols, long long n_pos, long
 int slices_override() {
     const char* s = std::getenv("TCSC_SLICES");
     return s ? std::atoi(s) : 0;
+}
+
+// TCSC_COMBINE_GIVEUP=1 (tests): in the in-launch combine every slice of a
+// tile except the last to arrive stops waiting at once, so the last arrival
+// reduces every band (the path a non-resident slice would take)
+int combine_giveup_knob() {
+    const char* s = std::getenv("TCSC_COMBINE_GIVEUP");
+    return s && std::atoi(s) != 0 ? 1 : 0;
 }
 
 // Workspace of one call = [X^T: xt_bytes(M, K)] [split-K slabs, if any].
@@ -532,8 +545,8 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
     if (stage == 1) return TCSC_OK;
     const bool prelu = is_prelu(variant);
     HIP_TRY(tcsc::mfma_gemm3(x3, p->w3, ldk, M, N, dB, dY, ldy, prelu, a, st));
-    HIP_TRY(tcsc::mfma_fixup(x3, M, K, ldk, p->ccp, p->ccn, p->crp, p->crn, N, dB, dY, ldy,
-                             variant == TCSC_VARIANT_BASIC, prelu, a, flags, st));
+    // fast order: bias after the sum for every variant
+    HIP_TRY(tcsc::mfma_fixup(x3, M, K, ldk, p->ccp, p->ccn, p->crm, N, dB, dY, ldy, false, prelu, a, flags, st));
     return TCSC_OK;
 }
 
@@ -562,9 +575,8 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
             HIP_TRY(hipMemcpyAsync(ws, dX, xb, hipMemcpyDeviceToDevice, st));
             return TCSC_OK;
         }
-        HIP_TRY(tcsc::launch_small_m(stage == 2 ? ws : dX, M, p->rows, p->ccp, p->ccn, p->crp, p->crn, p->cols, dB,
-                                     dY, ldy, variant == TCSC_VARIANT_BASIC, is_prelu(variant), a,
-                                     st));
+        HIP_TRY(tcsc::launch_small_m(stage == 2 ? ws : dX, M, p->rows, p->ccp, p->ccn, p->crm, p->cols, dB, dY, ldy,
+                                     false, is_prelu(variant), a, st));
         return TCSC_OK;
     }
     // gather-path limits: X^T row tiles of 64 rows on the transpose grid's y
@@ -628,21 +640,30 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
     g.ws_bytes = g.ws ? ws_bytes - xtb : 0;
     g.force_slices = force_slices > 0 ? force_slices : slices_override();
     g.stage = stage;
-    // the plan's own workspace (device API) with its synchronisation block:
-    // the fused persistent kernel (tcsc::launch_gemm decides if it applies)
-    if (ws == p->ws && p->fsync && M <= p->fsync_M) {
-        g.fsync = p->fsync;
-        g.fsync_n = tcsc::fused_sync_pairs(p->fsync_M, p->rows);
+    // the plan's own workspace (device API) with its combine words: the
+    // in-launch split-K combine (tcsc::launch_gemm decides if it applies)
+    if (ws == p->ws && p->csync) {
+        if (p->csync_dirty) {
+            HIP_TRY(hipMemsetAsync(p->csync, 0, tcsc::kCombineBytes, static_cast<hipStream_t>(stream)));
+            p->csync_dirty = false;
+        }
         g.num_cus = p->num_cus;
-        g.ccnt = tcsc::combine_words(p->fsync, p->fsync_M, p->rows);
+        g.ccnt = p->csync;
+        g.combine_giveup = combine_giveup_knob();
     }
-    // Bias first for tcsc_sgemm_basic (tcsc.c:74-96), last otherwise
-    // (tcsc.c:149-161; the optimized family adds per-sign partial sums to
-    // the bias, which no single accumulation order reproduces: DESIGN.md).
-    g.bias_first = (variant == TCSC_VARIANT_BASIC);
+    // The fast order (order 0) adds each column's nonzeros in ascending k and
+    // the bias after the sum for every variant: the reference's own dense
+    // oracle, dense.c:64-77 gemm_basic (y = 0; y += X*W; Y = y + B), bit for
+    // bit when K is not split.  The reference order adds the
+    // bias first for tcsc_sgemm_basic (tcsc.c:74-96) and sums the optimized
+    // family's signs apart (order 2).
+    g.bias_first = (g.order == 1 && variant == TCSC_VARIANT_BASIC);
     g.prelu = is_prelu(variant);
     hipError_t e = tcsc::launch_gemm(g, static_cast<hipStream_t>(stream));
-    if (e != hipSuccess) return hip_fail(e, "tcsc_gpu_sgemm launch");
+    if (e != hipSuccess) {
+        if (g.ccnt) p->csync_dirty = true;  // a partial launch may have left tile words set
+        return hip_fail(e, "tcsc_gpu_sgemm launch");
+    }
     return TCSC_OK;
 }
 }  // namespace
@@ -798,7 +819,7 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan* p) {
     if (p->ent) (void)hipFree(p->ent);
     if (p->sptr) (void)hipFree(p->sptr);
     if (p->ws) (void)hipFree(p->ws);
-    if (p->fsync) (void)hipFree(p->fsync);
+    if (p->csync) (void)hipFree(p->csync);
     free_mfma(p);
     free_csc(p);
     tcsc_gpu_plan_destroy(p->chain_pos);
@@ -818,19 +839,11 @@ int tcsc_gpu_plan_reserve(tcsc_gpu_plan* p, int max_M) {
                                           slices_override());
         want = std::max(want, tcsc::xt_bytes(max_M, p->rows) + tcsc::workspace_bytes(max_M, p->cols, s));
     }
-    if (max_M > p->fsync_M && p->rows > 0 && p->order == TCSC_ORDER_FAST) {
+    if (!p->csync && p->rows > 0 && p->order == TCSC_ORDER_FAST) {
         DeviceGuard dg(p->device);
-        if (p->fsync) {
-            HIP_TRY(hipDeviceSynchronize());  // a queued launch may still use it
-            (void)hipFree(p->fsync);
-            p->fsync = nullptr;
-            p->fsync_M = 0;
-        }
-        const size_t fb = tcsc::fused_sync_bytes(max_M, p->rows);
-        HIP_TRY(hipMalloc(&p->fsync, fb));
-        HIP_TRY(hipMemset(p->fsync, 0, fb));
+        HIP_TRY(hipMalloc(&p->csync, tcsc::kCombineBytes));
+        HIP_TRY(hipMemset(p->csync, 0, tcsc::kCombineBytes));
         HIP_TRY(hipDeviceSynchronize());
-        p->fsync_M = max_M;
         if (!p->num_cus) HIP_TRY(hipDeviceGetAttribute(&p->num_cus, hipDeviceAttributeMultiprocessorCount, p->device));
     }
     if (want <= p->ws_bytes) return TCSC_OK;
@@ -864,19 +877,8 @@ int tcsc_gpu_launch_info(const tcsc_gpu_plan* p, int M, int* path, int* slices) 
     }
     const int rows = std::min(M, 1 << 22);  // one launch of at most 2^22 rows (sgemm_ws)
     const size_t xtb = tcsc::xt_bytes(rows, p->rows);
-    tcsc::GemmArgs g;
-    g.X = reinterpret_cast<const float*>(p->ws);  // any 16-B aligned X
-    g.M = rows;
-    g.K = p->rows;
-    g.ncols = p->cols;
-    g.stage = 0;
-    g.order = p->order == TCSC_ORDER_REFERENCE ? 1 : 0;
-    if (p->fsync && rows <= p->fsync_M) {
-        g.fsync = p->fsync;
-        g.num_cus = p->num_cus;
-    }
-    *path = tcsc::fused_eligible(g) ? TCSC_PATH_FUSED : TCSC_PATH_GATHER;
-    if (g.order == 0)
+    *path = TCSC_PATH_GATHER;
+    if (p->order != TCSC_ORDER_REFERENCE)
         *slices = M > (1 << 22) ? 1
                                 : tcsc::choose_slices(rows, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups,
                                                       p->ws_bytes > xtb ? p->ws_bytes - xtb : 0, slices_override());
@@ -896,7 +898,7 @@ int tcsc_gpu_launch_combine(const tcsc_gpu_plan* p, int M, int* in_launch) {
     const int rows = std::min(M, 1 << 22);
     const int s = tcsc::normalized_slices(p->rows, slices);
     const long long cb = (p->n_groups + tcsc::kWaves - 1) / tcsc::kWaves, rt = (rows + tcsc::kTM - 1) / tcsc::kTM;
-    const bool words = p->fsync && rows <= p->fsync_M;
+    const bool words = p->csync != nullptr;
     *in_launch = tcsc::combine_applies(s, cb * rt * s, cb * rt, (long long)rows * p->cols, words ? p->num_cus : 0,
                                        words, p->cols % 4 == 0)
                      ? 1

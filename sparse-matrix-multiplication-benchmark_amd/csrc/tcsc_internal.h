@@ -162,105 +162,15 @@ struct PlanOut {
     size_t scan_tmp_bytes = 0;
 };
 
-// ---- the fused persistent gather (k_fused, DESIGN.md §4 "k_fused") --------
-// X^T is written by the same launch that gathers from it: the output tiles
-// (row tile rt, K slice z, column block cb) are items of a persistent grid,
-// grouped by (rt, z); the group's workgroups transpose its rows of X in
-// units a few pieces ahead of their own gather and count per piece of pc
-// chunks.  Two unit geometries (TCSC_FUSED_SMALL):
-//  * 0 (default): 4 k rows x 256 m (LDS-DMA of 4 x 1 KiB, 4 x 4 transpose in
-//    registers, four 1-KiB stores), one unit per step, made by waves 4-6;
-//  * 1: 1 k row x 64 m (one LDS-DMA dword per lane: 64 X rows, one
-//    ds_read_b32 and one 256-B store), batches of kSlotUnits per step, made
-//    by the 12 non-DMA waves 4-15, so that each wave's share per chunk is
-//    small.  Measured slower (cfg 4 1.84 against 1.46 ms: 16x the units,
-//    each as dear to issue), kept as an A/B build.
-#ifndef TCSC_FUSED_SMALL
-#define TCSC_FUSED_SMALL 0
-#endif
-#if TCSC_FUSED_SMALL
-constexpr int kUnitM = 64;                           // m per unit
-constexpr int kUnitsPerRow = kTM / kUnitM;           // 4 units per k row
-constexpr int kUnitsPerChunk = kTK * kUnitsPerRow;   // 192
-constexpr int kUnitBytes = kUnitM * 4;               // 256 B
-constexpr int kSlotUnits = 4;                        // units per producer step
-#ifndef TCSC_FUSED_PROD_WAVES
-#define TCSC_FUSED_PROD_WAVES 12
-#endif
-#else
-constexpr int kUnitK = 4;                        // k rows per transposition unit
-constexpr int kUnitsPerChunk = kTK / kUnitK;     // 12
-constexpr int kUnitBytes = kTM * kUnitK * 4;     // 4 KiB of LDS staging per unit
-constexpr int kSlotUnits = 1;
-static_assert(kTK % kUnitK == 0, "whole units per chunk");
-#ifndef TCSC_FUSED_PROD_WAVES
-#define TCSC_FUSED_PROD_WAVES 3
-#endif
-#endif
-// producer waves 4 .. 4+kProdWaves-1 (never the ring's DMA waves: the chunk
-// loop's vmcnt counts assume their VMEM ops); the poll wave is the first
-// producer in the small-unit geometry, the wave after the producers otherwise
-constexpr int kProdWave0 = 4;
-constexpr int kProdWaves = TCSC_FUSED_PROD_WAVES;
-constexpr int kPollWave = TCSC_FUSED_SMALL ? kProdWave0 : kProdWave0 + kProdWaves;
-static_assert(kProdWaves >= 1 && kProdWave0 + kProdWaves <= kWaves && kPollWave < kWaves, "producer and poll waves");
-static_assert(kProdWave0 >= kDmaWaves && kPollWave >= kDmaWaves, "producer and poll waves issue no ring DMAs");
-// LDS: the ring, one 256-B landing area that every wave's stream prefetch
-// shares (the data is never read), the producer slots, the item record
-constexpr int kFusedStateBytes = 64 + 16 * kProdWaves + 32;  // item record, producer hand-over words, 8 probe words
-constexpr int kProbeAhead = 4;         // chunks between a counter's probe and its check
-constexpr int kStoreDelay = 2;         // chunks from a unit's LDS-DMA to its stores
-constexpr int kSigDelay = 3;           // chunks from a unit's stores to its signal
-constexpr int kFusedPfOff = kRingBytes;
-constexpr int kFusedSlotOff = kFusedPfOff + 256;
-constexpr int kFusedStateOff = kFusedSlotOff + kProdWaves * kSlotUnits * kUnitBytes;
-constexpr int kFusedLdsBytes0 = kFusedStateOff + kFusedStateBytes;
-constexpr int kFusedProbeOff = kFusedStateOff + 64 + 16 * kProdWaves;
-constexpr int kFusedLdsBytes = kFusedLdsBytes0 > kEpiMinBytes ? kFusedLdsBytes0 : kEpiMinBytes;
-static_assert(kFusedLdsBytes <= 160 * 1024, "fused kernel LDS");
-// synchronisation block of a plan (device memory, zeroed once): [0] the
-// epoch of the last completed launch, [1] arrivals of the running launch,
-// then per (row tile, chunk) of the largest launch the block was sized for
-// two 32-bit piece counters, one per epoch parity (a launch counts on its
-// own set and zeroes the other for the next launch)
-constexpr size_t kFusedSyncHdr = 256;
-inline int fused_sync_pairs(int M, int K) {
-    const int nrt = (M + kTM - 1) / kTM, nch = (K + kTK - 1) / kTK;
-    return nrt * (nch > 0 ? nch : 1);
-}
-// + the in-launch split-K combine's tile words (k_stream OUT 2, after the
-// piece counters): per tile {arrivals, done, claims[Z]}, reset by the tile's
-// last workgroup, so every launch finds them zero
+// ---- the in-launch split-K combine's tile words (k_stream OUT 2) ----------
+// Per tile (row tile x column block) of a launch: {arrivals, done,
+// claims[Z]}, zeroed when the block is allocated and reset to zero by the
+// tile's last workgroup to finish, so every launch (and graph replay) finds
+// them at zero.  A launch that returns an error marks the block dirty and
+// the next launch on the plan re-zeroes it first (tcsc_api.cpp).
 constexpr int kCombineTiles = 256;
 constexpr int kCombineWords = 32;  // per tile: 2 + Z (Z <= 16) used
-inline size_t fused_sync_bytes(int M, int K) {
-    return kFusedSyncHdr + (size_t)fused_sync_pairs(M, K) * 8 + (size_t)kCombineTiles * kCombineWords * 4;
-}
-inline unsigned* combine_words(unsigned* sync, int M, int K) {
-    return sync ? reinterpret_cast<unsigned*>(reinterpret_cast<char*>(sync) + kFusedSyncHdr +
-                                              (size_t)fused_sync_pairs(M, K) * 8)
-                : nullptr;
-}
-
-struct FusedArgs {
-    const float* X = nullptr;       // M x K row-major
-    float* XT = nullptr;            // (K + look-ahead) x ldxt workspace
-    int M = 0, K = 0, ldxt = 0;
-    const int2* ent = nullptr;
-    const int* sptr = nullptr;
-    long long n_entries = 0;
-    int G = 0, ncols = 0, nch = 0, cps = 0, Z = 1, ncb = 0, n_items = 0;
-    const float* Bias = nullptr;
-    float* Y = nullptr;
-    int ldy = 0;
-    float a = 0.f;
-    float* ws = nullptr;            // split-K slabs (Z > 1)
-    int pf_dist = 0, pf_lines = 1;
-    unsigned* sync = nullptr;       // fused_sync_bytes(M, K) block
-    int pc = 8;                     // chunks per piece
-    int lead = 2;                   // pieces produced before an item's gather starts (~16 chunks' worth)
-    int sync_n = 0;                 // (row tile, chunk) counter pairs in the sync block
-};
+constexpr size_t kCombineBytes = (size_t)kCombineTiles * kCombineWords * 4;
 
 struct GemmArgs {
     const float* X = nullptr;
@@ -288,12 +198,9 @@ struct GemmArgs {
     size_t ws_bytes = 0;
     int force_slices = 0;      // 0 = cost model
     int stage = 0;             // 0: transpose + gather, 1: transpose only, 2: gather only (X^T prepared)
-    // stage 0 only: the plan's synchronisation block (fused_sync_bytes for at
-    // least this M) enables the fused persistent kernel; null = k_transpose + k_stream
-    unsigned* fsync = nullptr;
-    int fsync_n = 0;           // counter pairs in fsync (fused_sync_pairs of the size it was made for)
-    int num_cus = 0;           // persistent grid size (workgroups, one per CU)
-    unsigned* ccnt = nullptr;  // the split-K combine's tile words (combine_words of fsync)
+    int num_cus = 0;           // CUs of the device (the in-launch combine needs the grid resident)
+    unsigned* ccnt = nullptr;  // the split-K combine's tile words (kCombineBytes), null = k_reduce4
+    int combine_giveup = 0;    // test knob (TCSC_COMBINE_GIVEUP=1): every slice but the last arrival gives up at once
 };
 
 // Plan building
@@ -312,8 +219,6 @@ void pf_stream_params(long long n_entries, int n_groups, int n_chunks, int* dist
 size_t workspace_bytes(int M, int ncols, int slices);
 size_t xt_bytes(int M, int K);
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st);
-// whether launch_gemm takes the fused persistent kernel for these arguments
-bool fused_eligible(const GemmArgs& g);
 // tcsc_from_dense on the device
 // tile counts cp/cn ([row tile][col], dense_tile_rows(rows) rows per tile)
 // turned into per-column tile offsets in place; column totals into totp/totn
@@ -344,9 +249,12 @@ hipError_t launch_transpose(const float* X, int M, int K, float* XT, int ldxt, h
 
 // ---- per-column CSC copy of a plan's range (small-M path, MFMA fixup) ------
 // cp/cn (ncols+1) and crp/crn (n_pos/n_neg) <- columns [col_begin,
-// col_begin+ncols) of the absolute-offset arrays, rebased.
+// col_begin+ncols) of the absolute-offset arrays, rebased; crm (n_pos+n_neg)
+// <- each column's +1 and -1 rows merged in ascending order (the fast
+// order's), -1 rows tagged with bit 31, column j at cp[j] + cn[j].
 hipError_t csc_copy(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int ncols,
-                    long long n_pos, long long n_neg, int* cp, int* cn, int* crp, int* crn, hipStream_t st);
+                    long long n_pos, long long n_neg, int* cp, int* cn, int* crp, int* crn, int* crm,
+                    hipStream_t st);
 
 // ---- MFMA path for near-dense W (tcsc_mfma.hip) ------------
 // X3 / W3T rows are ldk = mfma_ldk(K) bf16 long, in blocks of kMfmaBlk = 32
@@ -370,11 +278,11 @@ hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const i
                          int ncols, float* wf, uint16_t* w3, int ldk, long long n_pos, long long n_neg, int* bad,
                          hipStream_t st);
 // ---- small-M path (tcsc_small.hip) ----------------------------
-// Y[m, j] = act(B[j] + sum_P X[m,k] - sum_Q X[m,k]) for m < M <= 16, one wave
-// per column over the CSC copy.
-hipError_t launch_small_m(const float* X, int M, int K, const int* cp, const int* cn, const int* crp, const int* crn,
-                          int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
-                          hipStream_t st);
+// Y[m, j] = act(sum over column j's merged rows of +-X[m,k], ascending k,
+// then + B[j]) for m < M <= 16: one lane per column over the merged CSC copy,
+// the fast order's exact arithmetic (bit-identical to k_stream unsplit).
+hipError_t launch_small_m(const float* X, int M, int K, const int* cp, const int* cn, const int* crm, int ncols,
+                          const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a, hipStream_t st);
 // X (M x K) -> x3 (M x ldk bf16, [h | m | l | 0..]); flags[m] = 1 for the
 // rows the fixup recomputes, 0 otherwise (every row, every call).
 hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int* flags, hipStream_t st);
@@ -382,9 +290,9 @@ hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int
 hipError_t mfma_gemm3(const uint16_t* x3, const uint16_t* w3, int ldk, int M, int N, const float* B, float* Y,
                       int ldy, bool prelu, float a, hipStream_t st);
 // Rewrites the flagged rows in k_stream's fast order (no-op when none is).
-hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cp, const int* cn, const int* crp,
-                      const int* crn, int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu,
-                      float a, const int* flags, hipStream_t st);
+hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cp, const int* cn, const int* crm,
+                      int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
+                      const int* flags, hipStream_t st);
 
 // Error channel shared by every entry point of the library (tcsc_api.cpp):
 // the message behind tcsc_gpu_last_error(), and the host API's policy

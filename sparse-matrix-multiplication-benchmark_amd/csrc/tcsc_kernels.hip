@@ -467,10 +467,20 @@ __device__ __forceinline__ Tile xcd_tile() {
 // read with tcsc_debug_stamps().  Stamps never feed an output.
 constexpr int kStampWgs = 4096;
 __device__ unsigned long long g_stamps[kStampWgs * kWaves * 4];
+// per workgroup (wave 0), s_memrealtime (100 MHz, one clock for the whole
+// chip): entry, chunk loop start, chunk loop end, epilogue end, kernel end
+__device__ unsigned long long g_wgtime[kStampWgs * 8];
 __device__ __forceinline__ unsigned long long stamp() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+__device__ __forceinline__ unsigned long long rtstamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     __builtin_amdgcn_sched_barrier(0);
     return t;
 }
@@ -486,8 +496,9 @@ __device__ __forceinline__ unsigned long long stamp() {
 // order as k_reduce4, so the same bits.  The workgroup whose add came last
 // knows the slabs are complete without polling; after its own band it
 // claims and reduces any band still unclaimed, so a workgroup whose poll
-// gives up (kCombineSpin polls: a slice that is not resident) leaves no band
-// undone, and no band is reduced twice.  The last workgroup to finish
+// gives up (after kCombineWaitTicks of wall time, ~50 us: a slice that is not
+// resident, or TCSC_COMBINE_GIVEUP) leaves no band undone, and no band is
+// reduced twice.  The last workgroup to finish
 // (the done word) zeroes the tile's words for the next launch.  The host
 // takes this path only when the grid fits the chip at one workgroup per CU
 // (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility",
@@ -496,7 +507,17 @@ __device__ __forceinline__ unsigned long long stamp() {
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4c_t __attribute__((ext_vector_type(4)));
 constexpr int kSc1 = 16;  // buffer cache-policy bits: sc1
-constexpr int kCombineSpin = 1 << 20;
+// The hand-off leans on gfx942/gfx950's lowering of sc1 loads and stores
+// (L1 bypassed, written through to the memory side) and of relaxed
+// agent-scope atomics; other targets would need the release/acquire fences
+// (DESIGN.md §4 k_reduce, the protocol and its conditions).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "combine_tile's sc1 hand-off is written for gfx942/gfx950 only"
+#endif
+// A slice waits for its tile's other slices at most this long (s_memrealtime
+// ticks, 100 MHz: 50 us, against a few us of measured slab skew); then it
+// leaves its band to the tile's last arrival.
+constexpr unsigned long long kCombineWaitTicks = 5000;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t slabs_rsrc(float* ws, int Z, int M, int ncols) {
     const long long bytes = (long long)Z * M * ncols * 4;
     return __builtin_amdgcn_make_buffer_rsrc(ws, 0, (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL), 0x00020000);
@@ -505,7 +526,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t slabs_rsrc(float* ws, int Z, i
 template <bool BIAS_FIRST, bool PRELU>
 __device__ __forceinline__ void combine_tile(float* ws, int M, int ncols, const float* __restrict__ Bias,
                                              float* __restrict__ Y, int ldy, float a, unsigned* ccnt, const Tile t,
-                                             char* lds) {
+                                             char* lds, int giveup) {
     const int Z = (int)gridDim.z;
     unsigned* w = ccnt + (size_t)(t.rt * (int)gridDim.x + t.cb) * kCombineWords;  // {arrivals, done, claims[Z]}
     int* flag = reinterpret_cast<int*>(lds);  // the epilogue's staging is done (barrier below)
@@ -514,11 +535,16 @@ __device__ __forceinline__ void combine_tile(float* ws, int M, int ncols, const 
     if (threadIdx.x == 0) {
         const unsigned old = __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int st = old + 1 == (unsigned)Z ? 2 : 0;  // 2: the last arrival, 1: saw all arrive, 0: gave up
-        for (int n = 0; st == 0 && n < kCombineSpin; ++n) {
-            if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)Z)
-                st = 1;
-            else
+        if (st == 0 && !giveup) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)Z) {
+                    st = 1;
+                    break;
+                }
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kCombineWaitTicks) break;
                 __builtin_amdgcn_s_sleep(4);
+            }
         }
         flag[0] = st;
     }
@@ -610,7 +636,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
          const int* __restrict__ sptr, long long n_entries, const int2* __restrict__ ent2,
          const int* __restrict__ sptr2, long long n_entries2, int G, int ncols, int nch, int chunks_per_slice,
          const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a, float* __restrict__ ws, int pf_dist,
-         int pf_lines, unsigned* __restrict__ ccnt) {
+         int pf_lines, unsigned* __restrict__ ccnt, int combine_giveup) {
     static_assert(ORDER == 0 || OUT == 0, "the reference orders do not split K");
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const int lane = threadIdx.x & 63;
@@ -621,6 +647,9 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     const int c_begin = t.z * chunks_per_slice;
     const int c_end = min(nch, c_begin + chunks_per_slice);
     const bool active = g < G;
+#ifdef TCSC_STAMPS
+    unsigned long long rt_[5] = {rtstamp(), 0, 0, 0, 0};
+#endif
 
     facc_t acc[TCSC_ACC_VECS];
 #pragma unroll
@@ -712,6 +741,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
 #ifdef TCSC_STAMPS
         unsigned long long st_g = 0, st_p = 0, st_w = 0, t2 = stamp();
         const unsigned long long t_begin = t2;
+        rt_[1] = rtstamp();
 #endif
         for (int c = c_begin; c < c_end; ++c) {
             // see the VMEM order above: ring of 3 keeps DMA(c+1) in flight
@@ -741,6 +771,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
 #endif
         }
 #ifdef TCSC_STAMPS
+        rt_[2] = rtstamp();
         if (lane == 0) {
             const int wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
             unsigned long long* o = g_stamps + ((size_t)(wg % kStampWgs) * kWaves + wave) * 4;
@@ -886,7 +917,18 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     run_chain(ent, sptr, n_entries);
     if constexpr (ORDER == 0) {
         epilogue(std::integral_constant<int, 0>{});
-        if constexpr (OUT == 2) combine_tile<BIAS_FIRST, PRELU>(ws, M, ncols, Bias, Y, ldy, a, ccnt, t, lds);
+#ifdef TCSC_STAMPS
+        rt_[3] = rtstamp();
+#endif
+        if constexpr (OUT == 2) combine_tile<BIAS_FIRST, PRELU>(ws, M, ncols, Bias, Y, ldy, a, ccnt, t, lds, combine_giveup);
+#ifdef TCSC_STAMPS
+        rt_[4] = rtstamp();
+        if (threadIdx.x == 0) {
+            const int wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+            if (wg < kStampWgs)
+                for (int i = 0; i < 5; ++i) g_wgtime[wg * 8 + i] = rt_[i];
+        }
+#endif
     } else if constexpr (ORDER == 1) {
         __syncthreads();  // every wave is done with the ring before the -1 chain refills it
         run_chain(ent2, sptr2, n_entries2);
@@ -901,910 +943,6 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         pad_rows();
         run_chain(ent2, sptr2, n_entries2);
         epilogue(std::integral_constant<int, 2>{});
-    }
-}
-
-// ---------------------------------------------------------------------------
-// K1f: k_fused -- the persistent gather with the X^T staging fused in
-// ---------------------------------------------------------------------------
-// One workgroup per CU (the grid is the chip's resident capacity) loops over
-// items (row tile rt, K slice z, column block cb) numbered group-major, item
-// = (rt*Z + z)*ncb + cb: the ncb items of one group (rt, z) -- the column
-// blocks that stream the same rows of X^T -- are consecutive and, through
-// the XCD-aware slot order, run at once on one XCD (the L2 sharing of
-// k_stream's tile order).  Instead of a k_transpose launch ahead of the
-// gather, the group's workgroups write its rows of X^T themselves while they
-// gather (the transpose is HBM-bound, the gather LDS-bound):
-//  * a unit is 4 k rows x 256 m: an LDS-DMA of 4 x 1 KiB (lane l: X rows
-//    m0+4l..4l+3, k0..k0+3) into a 4-KiB slot, ds_read_b128 x 4, a 4 x 4
-//    transpose in registers, 4 x global_store_dwordx4 sc1 (1-KiB rows of X^T);
-//  * the group's members (its items in the group's first round of the grid)
-//    have two producer agents each (waves 4 and 5); agent a of An produces
-//    the units u = a, a + An, ... of the group's K range; a piece is pc
-//    chunks (12*pc units); an agent adds 1 to a piece's counter once its
-//    units of the piece are stored and complete (s_waitcnt vmcnt, then an
-//    agent-scope atomic);
-//  * an item first produces its units of the first `lead` pieces (all of
-//    them when the group has too few members to stay ahead), then every
-//    producer wave produces one unit per chunk (the LDS-DMA issued after
-//    gather(c) is consumed after gather(c+1), one slot per wave after the
-//    ring);
-//  * before the barrier that precedes the DMA of a piece's first chunk, wave
-//    6 polls the piece's counter until it reads {this launch's epoch, the
-//    piece's agent count}; the barrier then orders every wave's loads of
-//    those rows after the poll (MI355X_MICROARCH.md, inter-workgroup
-//    visibility: sc1 stores drained by vmcnt, agent atomic, sc1 poll,
-//    workgroup barrier).
-// The counters carry the launch's epoch in their upper half and are never
-// reset: every workgroup reads the epoch of the last completed launch from
-// the plan's sync block at entry, and the last workgroup to finish (an
-// atomicInc that wraps back to 0) advances it, so a captured graph replays
-// correctly.  A wait longer than kPollLimit polls (a member that is not
-// resident: the GPU shared with another kernel) makes the waiting workgroup
-// produce the piece itself (the same values; writes are idempotent).
-constexpr int kPollLimit = 1 << 12;
-#ifndef TCSC_FUSED_DIAG_PURE  // timing diagnostic only (tools/ab.mk fpu): k_transpose first, no production or polls
-#define TCSC_FUSED_DIAG_PURE 0
-#endif
-#ifndef TCSC_FUSED_DIAG_NOLOOP  // timing diagnostic only (tools/ab.mk fnl): no in-loop production or polls
-#define TCSC_FUSED_DIAG_NOLOOP TCSC_FUSED_DIAG_PURE
-#endif
-// Timing diagnostic (tools/ab.mk fst, tools/fused_stamps.py): per workgroup,
-// s_memtime cycles of each item phase, of the producer steps that act, of
-// the poll wave's in-loop checks and of wave 0's chunk-barrier waits,
-// accumulated in LDS and added to g_fstamp at the end.
-#ifndef TCSC_FUSED_STAMPS
-#define TCSC_FUSED_STAMPS 0
-#endif
-#if TCSC_FUSED_STAMPS
-__device__ unsigned long long g_fstamp[4096 * 16];
-#define FST_NOW() ((unsigned long long)__builtin_amdgcn_s_memtime())
-#define FST_ADD(lds, slot, v)                                                                        \
-    do {                                                                                             \
-        if ((threadIdx.x & 63) == 0)                                                                 \
-            __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>((lds) + kFusedLdsBytes0) + (slot), \
-                                   (unsigned long long)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
-    } while (0)
-#else
-#define FST_NOW() 0ull
-#define FST_ADD(lds, slot, v) \
-    do {                      \
-        (void)(v);            \
-    } while (0)
-#endif
-
-__device__ __forceinline__ int xcd_slot(int b, int P) {
-    const int q = P >> 3, r = P & 7, x = b & 7;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
-}
-
-// Item schedule (TCSC_FUSED_XCD_RANGES, default): XCD x (the workgroups
-// b = x mod 8, MI355X_MICROARCH.md "Workgroup dispatch") takes a contiguous
-// range of the group-major item order, its Wx workgroups item base + j,
-// base + j + Wx, ...: a group's column blocks (one row tile of X^T) stay on
-// one XCD's L2 across rounds, as k_stream's tile order keeps them.  The
-// other schedule deals item slot + r*P (a group's items in one round, but
-// split over two XCDs, each reading the row tile into its own L2).
-#ifndef TCSC_FUSED_PF_SKIP  // producers skip the stream prefetch ahead of a signal step
-#define TCSC_FUSED_PF_SKIP TCSC_FUSED_SMALL
-#endif
-#ifndef TCSC_FUSED_ONE_ACTION  // A/B: at most one stage (signal, store or DMA) per producer step
-#define TCSC_FUSED_ONE_ACTION 1
-#endif
-#ifndef TCSC_FUSED_PROD_LATE  // A/B: producer steps after the gather instead of after the barrier
-#define TCSC_FUSED_PROD_LATE 0
-#endif
-#ifndef TCSC_FUSED_PROD_PRIO  // A/B: producer steps at raised wave priority
-#define TCSC_FUSED_PROD_PRIO 0
-#endif
-#ifndef TCSC_FUSED_XCD_RANGES
-#define TCSC_FUSED_XCD_RANGES 1
-#endif
-struct XcdRange {
-    int base, end, W;  // the XCD's items [base, end), its workgroups
-};
-__device__ __forceinline__ XcdRange xcd_range(int x, int P, int n_items) {
-    const int q = P >> 3, rr = P & 7;
-    const int W = q + (x < rr ? 1 : 0), pre = x * q + min(x, rr);
-    return XcdRange{(int)((long long)n_items * pre / P), (int)((long long)n_items * (pre + W) / P), W};
-}
-__device__ __forceinline__ int first_item(int b, int P, int n_items) {
-    if (!TCSC_FUSED_XCD_RANGES) return xcd_slot(b, P);
-    const XcdRange g = xcd_range(b & 7, P, n_items);
-    const int i = g.base + (b >> 3);
-    return i < g.end ? i : n_items;
-}
-__device__ __forceinline__ int next_item(int item, int b, int P, int n_items) {
-    if (!TCSC_FUSED_XCD_RANGES) return item + P;
-    const XcdRange g = xcd_range(b & 7, P, n_items);
-    const int i = item + g.W;
-    return i < g.end ? i : n_items;
-}
-// The end of the members of the group starting at gi0: the group's items that
-// run in the same round as gi0 (same XCD range and round, or round-robin round).
-__device__ __forceinline__ int members_end(int gi0, int ncb, int P, int n_items) {
-    if (!TCSC_FUSED_XCD_RANGES) return min(gi0 + ncb, (gi0 / P + 1) * P);
-    int x = 0;
-    XcdRange g = xcd_range(0, P, n_items);
-    while (x < 7 && gi0 >= g.end) g = xcd_range(++x, P, n_items);
-    const int round_end = g.base + ((gi0 - g.base) / g.W + 1) * g.W;
-    return min(min(gi0 + ncb, g.end), round_end);
-}
-
-// Piece counters: 32-bit, two sets used by alternate launches (epoch
-// parity); a launch zeroes the other set for the next one, so a signal is a
-// plain atomic add (no compare-and-swap retries among a piece's ~100 agents).
-__device__ __forceinline__ void piece_signal(unsigned* c) {
-    (void)__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ bool piece_ready(unsigned* c, unsigned tgt) {
-    const unsigned v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return (unsigned)__builtin_amdgcn_readfirstlane((int)v) >= tgt;
-}
-
-// Early probe of a piece counter (poll wave, a few chunks before the piece
-// is needed): one lane's sc1 LDS-DMA of the counter into an LDS word, so the
-// round trip overlaps the gather instead of stalling the chunk barrier.
-__device__ __forceinline__ void piece_probe(unsigned ldsw, const unsigned* c) {
-    unsigned sv;
-    asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %[m]\n\ts_nop 0\n\tglobal_load_lds_dword %[o], %[b] sc1\n\t"
-                 "s_mov_b32 m0, %[sv]"
-                 : [sv] "=&s"(sv)
-                 : [m] "s"(ldsw), [o] "v"(0u), [b] "s"(c)
-                 : "memory");
-}
-
-// LDS-DMA of unit (X rows m0 .. m0+255, k0 .. k0+3) into LDS at `slot`:
-// instruction r writes slot + r KiB, lane l X[min(m0+4l+r, M-1)][k0 .. k0+3].
-__device__ __forceinline__ void unit_dma(const float* X, int K, int M, int m0, int k0, unsigned slot, int lane) {
-    const char* base = reinterpret_cast<const char*>(X + (size_t)m0 * K + k0);
-    const int mmax = M - 1 - m0;
-    unsigned off[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) off[r] = (unsigned)min(4 * lane + r, mmax) * (unsigned)K * 4u;
-    unsigned sv;
-    asm volatile("s_mov_b32 %[sv], m0\n\t"
-                 "s_mov_b32 m0, %[s0]\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o0], %[b]\n\t"
-                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o1], %[b]\n\t"
-                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o2], %[b]\n\t"
-                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[o3], %[b]\n\t"
-                 "s_mov_b32 m0, %[sv]"
-                 : [sv] "=&s"(sv)
-                 : [s0] "s"(slot), [o0] "v"(off[0]), [o1] "v"(off[1]), [o2] "v"(off[2]), [o3] "v"(off[3]),
-                   [b] "s"(base)
-                 : "memory", "scc");
-}
-
-typedef float f32x4v __attribute__((ext_vector_type(4)));
-
-// Four global_store_dwordx4 sc1 (rows o, o+st, o+2st, o+3st of base) in one
-// asm block.  A store of more than 8 bytes still reads its data VGPRs in the
-// cycle after issue: a VALU write to them right after it corrupts the value
-// the last quarter-wave stores (the compiler's hazard recognizer does not
-// see stores inside inline asm), hence the trailing s_nop.
-__device__ __forceinline__ void store4_sc1(char* base, unsigned o, unsigned st, f32x4v r0, f32x4v r1, f32x4v r2,
-                                           f32x4v r3) {
-    asm volatile("global_store_dwordx4 %0, %4, %8 sc1\n\t"
-                 "global_store_dwordx4 %1, %5, %8 sc1\n\t"
-                 "global_store_dwordx4 %2, %6, %8 sc1\n\t"
-                 "global_store_dwordx4 %3, %7, %8 sc1\n\t"
-                 "s_nop 1"
-                 ::"v"(o), "v"(o + st), "v"(o + 2 * st), "v"(o + 3 * st), "v"(r0), "v"(r1), "v"(r2), "v"(r3),
-                   "s"(base)
-                 : "memory");
-}
-
-// X^T rows k0 .. k0+3, columns m0 .. m0+255 from the unit staged at lds + slot
-// (ds_read_b128 x 4, the 4 x 4 block of lane l transposed in registers,
-// 4 x global_store_dwordx4 sc1: write-through, so no L2 write-back is needed
-// before the piece is signalled).
-struct UnitRegs {
-    f32x4v x0, x1, x2, x3;
-};
-__device__ __forceinline__ UnitRegs unit_load(const char* lds_slot, int lane) {
-    const f32x4v* s = reinterpret_cast<const f32x4v*>(lds_slot) + lane;
-    return UnitRegs{s[0], s[64], s[128], s[192]};
-}
-__device__ __forceinline__ void unit_store_regs(const UnitRegs& u, float* XT, int ldxt, int m0, int k0, int lane) {
-    const f32x4v x0 = u.x0, x1 = u.x1, x2 = u.x2, x3 = u.x3;
-    char* base = reinterpret_cast<char*>(XT + (size_t)k0 * ldxt + m0);
-    const unsigned o = 16u * lane, st = (unsigned)ldxt * 4u;
-    const f32x4v r0 = {x0.x, x1.x, x2.x, x3.x}, r1 = {x0.y, x1.y, x2.y, x3.y};
-    const f32x4v r2 = {x0.z, x1.z, x2.z, x3.z}, r3 = {x0.w, x1.w, x2.w, x3.w};
-    store4_sc1(base, o, st, r0, r1, r2, r3);
-}
-__device__ __forceinline__ void unit_store(const char* lds_slot, float* XT, int ldxt, int m0, int k0, int lane) {
-    unit_store_regs(unit_load(lds_slot, lane), XT, ldxt, m0, k0, lane);
-}
-
-// The same unit through registers (the timeout path: one wave, no LDS).
-__device__ __forceinline__ void unit_direct(const float* X, int K, int M, float* XT, int ldxt, int m0, int k0,
-                                            int lane) {
-    const int mmax = M - 1 - m0;
-    f32x4v x[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-        x[r] = *reinterpret_cast<const f32x4v*>(X + (size_t)(m0 + min(4 * lane + r, mmax)) * K + k0);
-    char* base = reinterpret_cast<char*>(XT + (size_t)k0 * ldxt + m0);
-    const unsigned o = 16u * lane, st = (unsigned)ldxt * 4u;
-    const f32x4v r0 = {x[0].x, x[1].x, x[2].x, x[3].x}, r1 = {x[0].y, x[1].y, x[2].y, x[3].y};
-    const f32x4v r2 = {x[0].z, x[1].z, x[2].z, x[3].z}, r3 = {x[0].w, x[1].w, x[2].w, x[3].w};
-    store4_sc1(base, o, st, r0, r1, r2, r3);
-}
-
-// Unit u of an item (relative to the item's first k row k_lo), on the row
-// tile's X rows (Xr = X + m0*K, mmax = M-1-m0) and X^T columns (XTr = XT + m0).
-#if TCSC_FUSED_SMALL
-// Small units: k row k_lo + u/4, columns 64*(u%4) .. +63 of the row tile.
-// LDS-DMA: lane l loads X[64q + l][k] (one dword) to slot + 4l; store: the
-// 64 dwords as one 256-B X^T row piece (sc1; a 4-B store has no data hazard).
-__device__ __forceinline__ void unit_dma_u(const float* Xr, int K, int mmax, int k_lo, int u, unsigned slot,
-                                           int lane) {
-    const int k = k_lo + (u >> 2), q = u & 3;
-    const char* base = reinterpret_cast<const char*>(Xr + k);
-    const unsigned off = (unsigned)min(64 * q + lane, mmax) * (unsigned)K * 4u;
-    unsigned sv;
-    asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %[s0]\n\ts_nop 0\n\tglobal_load_lds_dword %[o], %[b]\n\t"
-                 "s_mov_b32 m0, %[sv]"
-                 : [sv] "=&s"(sv)
-                 : [s0] "s"(slot), [o] "v"(off), [b] "s"(base)
-                 : "memory");
-}
-__device__ __forceinline__ void unit_store_u(const char* slot, float* XTr, int ldxt, int k_lo, int u, int lane) {
-    const int k = k_lo + (u >> 2), q = u & 3;
-    const float v = reinterpret_cast<const float*>(slot)[lane];
-    char* dst = reinterpret_cast<char*>(XTr + (size_t)k * ldxt + 64 * q);
-    asm volatile("global_store_dword %0, %1, %2 sc1" ::"v"(4u * (unsigned)lane), "v"(v), "s"(dst) : "memory");
-}
-__device__ __forceinline__ void unit_direct_u(const float* Xr, int K, int mmax, float* XTr, int ldxt, int k_lo, int u,
-                                              int lane) {
-    const int k = k_lo + (u >> 2), q = u & 3;
-    const float v = Xr[(size_t)min(64 * q + lane, mmax) * K + k];
-    char* dst = reinterpret_cast<char*>(XTr + (size_t)k * ldxt + 64 * q);
-    asm volatile("global_store_dword %0, %1, %2 sc1" ::"v"(4u * (unsigned)lane), "v"(v), "s"(dst) : "memory");
-}
-#else
-__device__ __forceinline__ void unit_dma_u(const float* Xr, int K, int mmax, int k_lo, int u, unsigned slot,
-                                           int lane) {
-    unit_dma(Xr + k_lo + kUnitK * u, K, mmax + 1, 0, 0, slot, lane);
-}
-__device__ __forceinline__ void unit_store_u(const char* slot, float* XTr, int ldxt, int k_lo, int u, int lane) {
-    unit_store(slot, XTr + (size_t)(k_lo + kUnitK * u) * ldxt, ldxt, 0, 0, lane);
-}
-__device__ __forceinline__ void unit_direct_u(const float* Xr, int K, int mmax, float* XTr, int ldxt, int k_lo, int u,
-                                              int lane) {
-    unit_direct(Xr + k_lo + kUnitK * u, K, mmax + 1, XTr + (size_t)(k_lo + kUnitK * u) * ldxt, ldxt, 0, 0, lane);
-}
-#endif
-// units of the k rows [k_lo, k_hi)
-__host__ __device__ constexpr int units_of(int krows) {
-#if TCSC_FUSED_SMALL
-    return krows * kUnitsPerRow;
-#else
-    return (krows + kUnitK - 1) / kUnitK;
-#endif
-}
-
-// The kernel's arguments, re-read from the kernarg segment at each use
-// (s_load, scalar-cache hits): an opaque copy of the segment pointer keeps
-// the compiler from holding every field in SGPRs across the chunk loop, where
-// the gather pins 54 of them.
-typedef __attribute__((address_space(4))) const FusedArgs cFusedArgs;
-__device__ __forceinline__ cFusedArgs* fargs() {
-    cFusedArgs* p = (cFusedArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
-    asm volatile("" : "+s"(p));
-    return p;
-}
-
-// Item record in LDS (written by wave 0 at each item's start, read by the
-// producer and poll waves inside the chunk loop, so none of it is live in
-// registers across the gather): dwords
-//   0-1 X + m0*K (bytes)   2-3 XT + m0 (bytes)   4 K   5 M-1-m0   6 ldxt   7 k_lo
-//   8 U (units)   9 units per piece   10 An (agents)   11 epoch   12 log2(pc)   13 lead
-//   14-15 the counter of piece 0
-// Producer state (waves 4, 5), dwords: 0 next unit (INT_MAX: none left),
-// 1 unit in the slot (-1: none), 2 unit whose stores were issued last (-1).
-struct ItemRec {
-    unsigned long long xrow, xtrow;
-    int K, mmax, ldxt, k_lo, U, upc, An;
-    unsigned e;
-    int pcs, lead;  // log2(chunks per piece), pieces produced in the item prologue
-    unsigned long long crow;  // this launch's counter of piece 0 (stride 2 words per chunk)
-};
-static_assert(sizeof(ItemRec) == 64, "item record layout");
-
-__device__ __forceinline__ ItemRec load_rec(const char* lds) {
-    const int4* q = reinterpret_cast<const int4*>(lds + kFusedStateOff);
-    const int4 a = q[0], b = q[1], c = q[2], d = q[3];
-    ItemRec r;
-    r.xrow = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(a.y) << 32) |
-             (unsigned)__builtin_amdgcn_readfirstlane(a.x);
-    r.xtrow = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(a.w) << 32) |
-              (unsigned)__builtin_amdgcn_readfirstlane(a.z);
-    r.K = __builtin_amdgcn_readfirstlane(b.x);
-    r.mmax = __builtin_amdgcn_readfirstlane(b.y);
-    r.ldxt = __builtin_amdgcn_readfirstlane(b.z);
-    r.k_lo = __builtin_amdgcn_readfirstlane(b.w);
-    r.U = __builtin_amdgcn_readfirstlane(c.x);
-    r.upc = __builtin_amdgcn_readfirstlane(c.y);
-    r.An = __builtin_amdgcn_readfirstlane(c.z);
-    r.e = (unsigned)__builtin_amdgcn_readfirstlane(c.w);
-    r.pcs = __builtin_amdgcn_readfirstlane(d.x);
-    r.lead = __builtin_amdgcn_readfirstlane(d.y);
-    r.crow = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(d.w) << 32) |
-             (unsigned)__builtin_amdgcn_readfirstlane(d.z);
-    return r;
-}
-
-// One production step of a producer wave, at chunk t of the item (relative
-// to its first chunk).  An agent's units move through three stages in batches
-// of kSlotUnits (ProdState, in registers: next unit, the batch in the LDS
-// slot and when its DMA was issued, the batch stored and when):
-//   DMA: unit u of piece p is issued once t >= (p - lead) * pc, i.e. about
-//        lead pieces ahead of the chunk that polls p -- production keeps a
-//        fixed distance ahead of the gather instead of racing it (racing
-//        makes every producer wave wait on its own stores each chunk, and the
-//        barrier makes the whole workgroup wait with it);
-//   store: kStoreDelay chunks later (an LDS-DMA from HBM takes ~1.1 us to
-//        land, more than a chunk), transposed and stored;
-//   signal: kSigDelay chunks after the stores, which have completed by then,
-//        so the s_waitcnt costs nothing; the piece's counter is bumped when
-//        this was the agent's last unit of the piece.
-// `drain` (after the chunk loop) moves every stage at once.  Returns the
-// next chunk at which a stage can move (the caller skips the step until
-// then: no LDS read per chunk), INT_MAX once the wave has nothing left.
-struct ProdState {
-    int u_next;    // the agent's next unit (INT_MAX: none left)
-    int d_u, d_n;  // first unit and count of the batch in the LDS slot (d_u -1: none)
-    int s_u, s_n;  // first unit and count of the batch stored, not yet signalled
-    int tD, tS;    // chunks of the batch's DMA and stores
-    int pf_n;      // stream prefetches issued since the last DMA (saturates at kStoreDelay)
-};
-
-__device__ __forceinline__ int prod_next_t(const ProdState& ps, int U, int upc, int lead, int pcs, int t) {
-    int tn = 0x7fffffff;
-    if (ps.s_u >= 0) tn = min(tn, ps.tS + kSigDelay);
-    if (ps.d_u >= 0) tn = min(tn, ps.tD + kStoreDelay);
-    else if (ps.u_next < U) tn = min(tn, (ps.u_next / upc - lead) << pcs);
-    return max(tn, t + 1);
-}
-
-__device__ __forceinline__ int produce_step(char* lds, int wave, int lane, int t, bool drain, ProdState& ps,
-                                            const ItemRec& r) {
-    if (ps.u_next == 0x7fffffff && ps.d_u < 0 && ps.s_u < 0) return 0x7fffffff;
-    const char* slot_ptr = lds + kFusedSlotOff + (wave - kProdWave0) * (kSlotUnits * kUnitBytes);
-    const unsigned long long q1 = FST_NOW();
-    const bool sig_now = ps.s_u >= 0 && (drain || t >= ps.tS + kSigDelay);
-    bool store_now = ps.d_u >= 0 && (ps.s_u < 0 || sig_now) && (drain || t >= ps.tD + kStoreDelay);
-    bool dma_now = (ps.d_u < 0 || store_now) && ps.u_next < r.U &&
-                   (drain || t >= ((ps.u_next / r.upc - r.lead) << r.pcs));
-#if TCSC_FUSED_ONE_ACTION
-    // one stage per step (a step then fits the wave's slack at the barrier):
-    // the signal first, then the store, then the DMA
-    if (!drain) {
-        if (sig_now) store_now = false;
-        if (sig_now || store_now) dma_now = false;
-    }
-#endif
-    if (!sig_now && !store_now && !dma_now) return prod_next_t(ps, r.U, r.upc, r.lead, r.pcs, t);
-    // A signal needs this wave's stores complete: vmcnt(0) (the guide's
-    // hand-off rule); they are >= kSigDelay chunks old, so it waits at most
-    // for the last chunk's stream prefetch (which TCSC_FUSED_PF_SKIP skips).  A store needs the slot's LDS-DMA landed: it is older
-    // than the pf_n stream prefetches issued since, and loads return in
-    // order, so vmcnt(pf_n) suffices and those prefetches stay in flight.
-    if (drain || sig_now)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (store_now) {
-        if (kPfS && ps.pf_n >= 2)
-            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else if (kPfS && ps.pf_n == 1)
-            asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    const unsigned long long q2 = FST_NOW();
-    FST_ADD(lds, 9, q2 - q1);
-    if (sig_now) {
-        unsigned* crow = reinterpret_cast<unsigned*>(r.crow);
-#pragma unroll
-        for (int i = 0; i < kSlotUnits; ++i) {
-            const int u = ps.s_u + i * r.An;
-            const int p = u / r.upc;
-            if (i < ps.s_n && u + r.An >= min(r.U, (p + 1) * r.upc) && lane == 0)
-                piece_signal(crow + ((size_t)p << (r.pcs + 1)));
-        }
-        ps.s_u = -1;
-    }
-    const unsigned long long q3 = FST_NOW();
-    FST_ADD(lds, 12, q3 - q2);
-    if (store_now) {
-        float* XTr = reinterpret_cast<float*>(r.xtrow);
-#pragma unroll
-        for (int i = 0; i < kSlotUnits; ++i)
-            if (i < ps.d_n) unit_store_u(slot_ptr + i * kUnitBytes, XTr, r.ldxt, r.k_lo, ps.d_u + i * r.An, lane);
-        ps.s_u = ps.d_u;
-        ps.s_n = ps.d_n;
-        ps.tS = t;
-        ps.d_u = -1;
-    }
-    const unsigned long long q4 = FST_NOW();
-    FST_ADD(lds, 10, q4 - q3);
-    if (dma_now) {
-        const float* Xr = reinterpret_cast<const float*>(r.xrow);
-        ps.d_u = ps.u_next;
-        int n = 0;
-#pragma unroll
-        for (int i = 0; i < kSlotUnits; ++i)
-            if (ps.u_next < r.U) {
-                unit_dma_u(Xr, r.K, r.mmax, r.k_lo, ps.u_next,
-                           (unsigned)reinterpret_cast<uintptr_t>(slot_ptr) + i * kUnitBytes, lane);
-                ps.u_next += r.An;
-                ++n;
-            }
-        ps.d_n = n;
-        if (ps.u_next >= r.U) ps.u_next = 0x7fffffff;
-        ps.tD = t;
-        ps.pf_n = 0;
-    }
-    FST_ADD(lds, 11, FST_NOW() - q4);
-    if (ps.u_next == 0x7fffffff && ps.d_u < 0 && ps.s_u < 0) return 0x7fffffff;
-    return prod_next_t(ps, r.U, r.upc, r.lead, r.pcs, t);
-}
-
-// Wave 6 before the barrier ahead of chunk c+kNBuf-1's DMA: when that chunk
-// opens a piece, wait until the piece's counter is complete.  Past
-// kPollLimit polls (a member that is not running) the wave writes the
-// piece's X^T rows itself.
-__device__ __forceinline__ void wait_piece(const char* lds, int p, int lane, bool probed) {
-    const ItemRec r = load_rec(lds);
-    unsigned* c = reinterpret_cast<unsigned*>(r.crow) + ((size_t)p << (r.pcs + 1));
-    const unsigned tgt = (unsigned)min(r.An, min(r.U, (p + 1) * r.upc) - p * r.upc);
-    if (probed) {  // the probe issued kProbeAhead chunks ago (all but the last stream prefetch are done)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPfS ? 1 : 0) : "memory");
-        const unsigned v = reinterpret_cast<const volatile unsigned*>(lds + kFusedProbeOff)[p & 7];
-        if ((unsigned)__builtin_amdgcn_readfirstlane((int)v) >= tgt) return;
-    }
-    for (int n = 0; !piece_ready(c, tgt); ++n) {
-        if (n > kPollLimit) {
-            const float* Xr = reinterpret_cast<const float*>(r.xrow);
-            float* XTr = reinterpret_cast<float*>(r.xtrow);
-            const int u1 = min(r.U, (p + 1) * r.upc);
-            for (int u = p * r.upc; u < u1; ++u) unit_direct_u(Xr, r.K, r.mmax, XTr, r.ldxt, r.k_lo, u, lane);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            return;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-}
-
-// Poll wave, right after a chunk barrier (the LDS queue is short then):
-// whether piece pc_next (checked before the next barrier; -1: none) is
-// complete by its probe, and the probe of piece pp (-1: none) for the check
-// kProbeAhead chunks later.  One LDS round trip for the record and the word.
-__device__ __forceinline__ bool poll_after_barrier(const char* lds, int pc_next, bool probed, int pp, int pcs,
-                                                   int lane) {
-    const int4* rec = reinterpret_cast<const int4*>(lds + kFusedStateOff);
-    if (pc_next >= 0 && probed)  // the probe is >= kProbeAhead - 1 chunks old: all but the last stream prefetch
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPfS ? 1 : 0) : "memory");
-    const int4 c2 = rec[2], c3 = rec[3];
-    const unsigned v = reinterpret_cast<const volatile unsigned*>(lds + kFusedProbeOff)[(pc_next < 0 ? 0 : pc_next) & 7];
-    bool ready = true;
-    if (pc_next >= 0) {
-        ready = false;
-        if (probed) {
-            const int U = __builtin_amdgcn_readfirstlane(c2.x), upc = __builtin_amdgcn_readfirstlane(c2.y),
-                      An = __builtin_amdgcn_readfirstlane(c2.z);
-            const unsigned tgt = (unsigned)min(An, min(U, (pc_next + 1) * upc) - pc_next * upc);
-            ready = (unsigned)__builtin_amdgcn_readfirstlane((int)v) >= tgt;
-        }
-    }
-    if (pp >= 0) {
-        const unsigned long long cr = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(c3.w) << 32) |
-                                      (unsigned)__builtin_amdgcn_readfirstlane(c3.z);
-        const unsigned* c = reinterpret_cast<const unsigned*>(cr) + ((size_t)pp << (pcs + 1));
-        if (lane == 0)
-            piece_probe((unsigned)reinterpret_cast<uintptr_t>(lds) + kFusedProbeOff + 4u * (unsigned)(pp & 7), c);
-    }
-    return ready;
-}
-
-// Poll wave, kProbeAhead chunks before the check of piece p: the probe of
-// its counter.
-__device__ __forceinline__ void probe_issue(const char* lds, int p, int pcs, int lane) {
-    const int* rec = reinterpret_cast<const int*>(lds + kFusedStateOff);
-    const unsigned long long cr = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(rec[15]) << 32) |
-                                  (unsigned)__builtin_amdgcn_readfirstlane(rec[14]);
-    const unsigned* c = reinterpret_cast<const unsigned*>(cr) + ((size_t)p << (pcs + 1));
-    if (lane == 0)
-        piece_probe((unsigned)reinterpret_cast<uintptr_t>(lds) + kFusedProbeOff + 4u * (unsigned)(p & 7), c);
-}
-
-// Opaque copies: the value is the same, but the compiler cannot hoist what
-// is derived from it out of the loop it is made in.  k_fused makes its lane
-// and wave numbers opaque at the start of every phase of an item, so values
-// a phase derives from them are computed in that phase instead of before the
-// item loop (where they would stay live across every gather: spills).
-__device__ __forceinline__ int opaque_v(int x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-__device__ __forceinline__ int opaque_s(int x) {
-    asm volatile("" : "+s"(x));
-    return x;
-}
-
-struct ItemPos {
-    int rt, z, cb, grp, m0, c_begin, c_end;
-};
-__device__ __forceinline__ ItemPos item_pos(int item) {
-    cFusedArgs* F = fargs();
-    ItemPos q;
-    q.grp = item / F->ncb;
-    q.cb = item - q.grp * F->ncb;
-    q.rt = q.grp / F->Z;
-    q.z = q.grp - q.rt * F->Z;
-    q.m0 = q.rt * kTM;
-    q.c_begin = q.z * F->cps;
-    q.c_end = min(F->nch, q.c_begin + F->cps);
-    return q;
-}
-
-template <bool BIAS_FIRST, bool PRELU, int OUT>
-__global__ void __launch_bounds__(kWaves * 64, kWavesPerSimd) k_fused(const FusedArgs A) {
-    __shared__ __attribute__((aligned(16))) char lds[kFusedLdsBytes + (TCSC_FUSED_STAMPS ? 128 : 0)];
-    (void)A;  // every field is read through fargs()
-#if TCSC_FUSED_STAMPS
-    if (threadIdx.x < 16) reinterpret_cast<unsigned long long*>(lds + kFusedLdsBytes0)[threadIdx.x] = 0;
-    __syncthreads();
-#endif
-    {
-        // the epoch of this launch: the last completed launch's + 1
-        unsigned* sync = fargs()->sync;
-        const unsigned e = (unsigned)__builtin_amdgcn_readfirstlane(
-            (int)(__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u));
-        if (threadIdx.x == 0) reinterpret_cast<unsigned*>(lds + kFusedStateOff)[11] = e;
-        // zero the other set of piece counters for the next launch (this
-        // launch uses set e & 1 only; the kernel boundary orders the stores)
-        unsigned* cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(sync) + kFusedSyncHdr) + (~e & 1u);
-        const int n = fargs()->sync_n;
-        for (int i = blockIdx.x * (int)blockDim.x + (int)threadIdx.x; i < n; i += (int)(gridDim.x * blockDim.x))
-            cnt[2 * (size_t)i] = 0u;
-    }
-
-    for (int item = first_item(blockIdx.x, gridDim.x, fargs()->n_items); item < fargs()->n_items;
-         item = opaque_s(next_item(item, blockIdx.x, gridDim.x, fargs()->n_items))) {
-        // ---- item prologue: this agent's units of the first `lead` pieces, the record, piece 0 ----
-        const unsigned long long fst0 = FST_NOW();
-        {
-            const int lane = opaque_v(threadIdx.x & 63);
-            const int wave = opaque_s(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
-            const bool prod_wave = wave >= kProdWave0 && wave < kProdWave0 + kProdWaves;
-            const int P = gridDim.x;
-            const ItemPos q = item_pos(item);
-            cFusedArgs* F = fargs();
-            const int ncb = F->ncb, nch = F->nch, K = F->K, M = F->M;
-            // the group's members: its items in the group's first round
-            const int gi0 = q.grp * ncb;
-            const int mem_end = members_end(gi0, ncb, P, F->n_items);
-            const int An = kProdWaves * (mem_end - gi0);
-            const int k_lo = q.c_begin * kTK;
-            const int U = q.c_begin < q.c_end ? units_of(min(q.c_end * kTK, K) - k_lo) : 0;
-            const int pc = F->pc, upc = kUnitsPerChunk * pc;
-            const int npieces = (U + upc - 1) / upc;
-            // every piece up front when the members cannot keep ahead (an agent
-            // moves kSlotUnits units per kSigDelay chunks at most; the group needs
-            // kUnitsPerChunk per chunk, with 20 % margin)
-            const int lead = (An * kSlotUnits * 5 < kSigDelay * kUnitsPerChunk * 6) ? npieces : min(F->lead, npieces);
-            const int agent = (!TCSC_FUSED_DIAG_PURE && item < mem_end && prod_wave) ? kProdWaves * (item - gi0) + (wave - kProdWave0) : -1;
-            unsigned* const crow0 = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(F->sync) + kFusedSyncHdr) +
-                                    2 * ((size_t)q.rt * nch + q.c_begin);
-            const float* Xr = F->X + (size_t)q.m0 * K;
-            float* XTr = F->XT + q.m0;
-            const int ldxt = F->ldxt;
-            __syncthreads();  // the previous item's epilogue is done with the LDS
-            int4* rec4 = reinterpret_cast<int4*>(lds + kFusedStateOff);
-            const unsigned e = (unsigned)__builtin_amdgcn_readfirstlane(rec4[2].w);
-            unsigned* const crow = crow0 + (e & 1u);  // this launch's set
-            int u_next = agent;
-            if (agent >= 0) {
-                const int lead_units = min(U, lead * upc);
-                constexpr int half = kRingBytes / kProdWaves / kUnitBytes;  // ring slots per producer wave
-                const int slot0 = (wave - kProdWave0) * half * kUnitBytes;
-                while (u_next < lead_units) {
-                    int nb = 0;
-                    for (int u = u_next; u < lead_units && nb < half; u += An, ++nb)
-                        unit_dma_u(Xr, K, M - 1 - q.m0, k_lo, u,
-                                   (unsigned)reinterpret_cast<uintptr_t>(lds) + slot0 + nb * kUnitBytes, lane);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    for (int i = 0; i < nb; ++i, u_next += An)
-                        unit_store_u(lds + slot0 + i * kUnitBytes, XTr, ldxt, k_lo, u_next, lane);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0)
-                    for (int p = 0; p < lead; ++p) {
-                        const int f = p * upc + (((agent - p * upc) % An) + An) % An;  // the agent's first unit in p
-                        if (f < min(U, (p + 1) * upc)) piece_signal(crow + 2 * (size_t)p * pc);
-                    }
-            }
-            if (prod_wave && lane == 0)
-                reinterpret_cast<int4*>(lds + kFusedStateOff + 64)[wave - kProdWave0] =
-                    make_int4(agent >= 0 && u_next < U ? u_next : 0x7fffffff, -1, -1, 0);
-            if (wave == 0 && lane == 0) {
-                const unsigned long long xr = reinterpret_cast<unsigned long long>(Xr);
-                const unsigned long long xtr = reinterpret_cast<unsigned long long>(XTr);
-                const unsigned long long cr = reinterpret_cast<unsigned long long>(crow);
-                rec4[0] = make_int4((int)xr, (int)(xr >> 32), (int)xtr, (int)(xtr >> 32));
-                rec4[1] = make_int4(K, M - 1 - q.m0, ldxt, k_lo);
-                rec4[2] = make_int4(U, upc, An, (int)e);
-                rec4[3] = make_int4(31 - __builtin_clz(pc), lead, (int)cr, (int)(cr >> 32));
-            }
-            __syncthreads();  // the record, before the first wait
-            if (!TCSC_FUSED_DIAG_PURE && wave == kPollWave && npieces > 0) wait_piece(lds, 0, lane, false);
-            __syncthreads();
-        }
-        const unsigned long long fst1 = FST_NOW();
-        if (threadIdx.x < 64) FST_ADD(lds, 0, fst1 - fst0);
-
-        facc_t acc[TCSC_ACC_VECS];
-#pragma unroll
-        for (int v = 0; v < TCSC_ACC_VECS; ++v)
-#pragma unroll
-            for (int i = 0; i < TCSC_ACC_W; ++i) acc[v][i] = 0.f;
-
-        // ---- the chunk loop (k_stream's) ----
-        {
-            const int lane = opaque_v(threadIdx.x & 63);
-            const int wave = opaque_s(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
-            const ItemPos q = item_pos(item);
-            const int g = q.cb * kWaves + wave;
-            cFusedArgs* F = fargs();
-            const bool active = g < F->G;
-            if (BIAS_FIRST && OUT == 0 && active) {
-                const int cbias = group_col0(g) + lane;
-                const float bv = (lane < wave_cols(wave) && cbias < F->ncols) ? F->Bias[cbias] : 0.f;
-#pragma unroll
-                for (int j = 0; j < kCW; ++j) {
-                    const float b = __shfl(bv, j);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) acc_set(acc, 4 * j + r, b);
-                }
-            }
-            // the -0.0 pad row of every ring buffer (the prologue's production used the ring)
-            if (threadIdx.x < 64 * kNBuf) {
-                const int b = threadIdx.x >> 6;
-                reinterpret_cast<float4*>(lds + (b * kBufRows + kTK) * kRowBytes)[lane] =
-                    make_float4(-0.f, -0.f, -0.f, -0.f);
-            }
-            const int c_begin = q.c_begin, c_end = q.c_end;
-            if (c_begin < c_end) {
-                const bool prod_wave = wave >= kProdWave0 && wave < kProdWave0 + kProdWaves;
-                DmaState dma;
-                const int ldxt = F->ldxt;
-                dma.chunk_bytes = (size_t)kTK * ldxt * 4;
-                dma.next = reinterpret_cast<const char*>(F->XT + (size_t)c_begin * kTK * ldxt + q.m0);
-#pragma unroll
-                for (int i = 0; i < kDmaPerWave; ++i)
-                    dma.voff[i] = 16u * lane + (unsigned)((wave * kDmaPerWave + i) * ldxt * 4) -
-                                  (TCSC_DMA_OFFSET ? (unsigned)((i % 4) * kRowBytes) : 0u);
-                dma.lds_wave = (unsigned)reinterpret_cast<uintptr_t>(lds) + (unsigned)(wave * kDmaPerWave * kRowBytes);
-                const bool dma_wave = wave < kDmaWaves;
-                const int buf0 = c_begin % kNBuf;
-                const unsigned pf_m0 = (unsigned)reinterpret_cast<uintptr_t>(lds) + kFusedPfOff;
-                const unsigned pf_s_off = (unsigned)F->pf_dist + 128u * (unsigned)(lane * F->pf_lines >> 6);
-                // (a vector load: the kernel stores to global memory, so the
-                // compiler cannot prove sptr unchanged for a scalar load)
-                const long long s0 =
-                    active ? (long long)__builtin_amdgcn_readfirstlane(F->sptr[(long long)g * F->nch + c_begin])
-                           : F->n_entries;
-                unsigned long long cur = reinterpret_cast<unsigned long long>(F->ent + s0);
-                auto pf_issue = [&](unsigned long long p) {
-                    if (kPfS) pf_touch(pf_m0, pf_s_off, reinterpret_cast<const char*>(p));
-                };
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // pad rows
-                if (dma_wave) dma_next_chunk(dma, buf0);
-                i32x16 sb[TCSC_SBUF_VECS];
-                sbuf_tail_t sbt;
-                load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
-                pf_issue(cur);
-#pragma unroll
-                for (int i = 1; i + 1 < kNBuf; ++i) {
-                    if (dma_wave) dma_next_chunk(dma, (buf0 + i) % kNBuf);
-                    pf_issue(cur);
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                const unsigned mask = 0x3ffu;
-                int dbuf = (buf0 + kNBuf - 1) % kNBuf;
-                // per-wave event state in SGPRs (no LDS read per chunk): log2(pc)
-                // for the poll wave, the next chunk a producer wave can act at
-                const int pcs = opaque_s(__builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(lds + kFusedStateOff)[12]));
-                int t_evt = 0;
-                ProdState ps{0x7fffffff, -1, 0, -1, 0, 0, 0, 0};
-                // the item record in registers for the loop (a producer step or a
-                // poll then reads no LDS for it: the gather keeps the LDS queue long)
-                const ItemRec rec = load_rec(lds);
-                if (prod_wave) {  // the item prologue's hand-over: the agent's next unit
-                    const int4 st = reinterpret_cast<const int4*>(lds + kFusedStateOff + 64)[wave - kProdWave0];
-                    ps.u_next = __builtin_amdgcn_readfirstlane(st.x);
-                }
-                bool ready = false;  // poll wave: the next check's piece was seen complete after the last barrier
-                const int nloc = c_end - c_begin, pmask = (1 << pcs) - 1;
-                for (int c = c_begin; c < c_end; ++c) {
-                    const int t = c - c_begin;
-                    if (!TCSC_FUSED_DIAG_NOLOOP && wave == kPollWave) {  // chunk t+kNBuf-1 is DMA'd right after this barrier
-                        const int t2 = t + kNBuf - 1;
-                        if (t2 < nloc && (t2 & pmask) == 0 && !ready) {
-                            const unsigned long long w0 = FST_NOW();
-                            wait_piece(lds, t2 >> pcs, lane, false);
-                            FST_ADD(lds, 4, FST_NOW() - w0);
-                            FST_ADD(lds, 5, 1);
-                        }
-                    }
-#if TCSC_FUSED_STAMPS
-                    const unsigned long long b0 = FST_NOW();
-#endif
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kNBuf - 2) * kDmaPerWave + (kPfS ? 2 : 0)) : "memory");
-                    __builtin_amdgcn_s_barrier();
-#if TCSC_FUSED_STAMPS
-                    if (wave == 0) FST_ADD(lds, 6, FST_NOW() - b0);
-#endif
-                    if (dma_wave) dma_next_chunk(dma, dbuf);
-                    // producer and poll work right after the barrier, while the LDS queue is short
-                    if (!TCSC_FUSED_DIAG_NOLOOP && !TCSC_FUSED_PROD_LATE && prod_wave && t >= t_evt) {
-                        const unsigned long long p0 = FST_NOW();
-                        if (TCSC_FUSED_PROD_PRIO) __builtin_amdgcn_s_setprio(3);
-                        t_evt = produce_step(lds, wave, opaque_v(lane), t, false, ps, rec);
-                        if (TCSC_FUSED_PROD_PRIO) __builtin_amdgcn_s_setprio(0);
-                        FST_ADD(lds, 3, FST_NOW() - p0);
-                        FST_ADD(lds, 7, 1);
-                    }
-                    if (!TCSC_FUSED_DIAG_NOLOOP && wave == kPollWave) {
-                        const int tn = t + kNBuf;                 // the check before the next barrier
-                        const int tp = t + kNBuf - 1 + kProbeAhead;  // the probe for the check kProbeAhead chunks on
-                        const bool chk = tn < nloc && (tn & pmask) == 0;
-                        const bool prb = tp < nloc && (tp & pmask) == 0;
-                        ready = true;
-                        if (chk || prb)
-                            ready = poll_after_barrier(lds, chk ? tn >> pcs : -1, tn >= kNBuf - 1 + kProbeAhead,
-                                                       prb ? tp >> pcs : -1, pcs, opaque_v(lane));
-                    }
-                    gather_stream(sb, sbt, cur, lane, mask, acc);
-                    load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
-                    if (!TCSC_FUSED_DIAG_NOLOOP && TCSC_FUSED_PROD_LATE && prod_wave && t >= t_evt) {
-                        if (TCSC_FUSED_PROD_PRIO) __builtin_amdgcn_s_setprio(3);
-                        t_evt = produce_step(lds, wave, opaque_v(lane), t, false, ps, rec);
-                        if (TCSC_FUSED_PROD_PRIO) __builtin_amdgcn_s_setprio(0);
-                    }
-                    // a producer skips its stream prefetch ahead of a signal step, whose
-                    // vmcnt(0) would otherwise wait for it; it counts the ones it issues
-                    // (a store step's wait leaves that many in flight)
-                    if (!(TCSC_FUSED_PF_SKIP && prod_wave && ps.s_u >= 0 && t + 1 >= ps.tS + kSigDelay)) {
-                        pf_issue(cur);
-                        ps.pf_n = min(ps.pf_n + 1, kStoreDelay);
-                    }
-                    dbuf = dbuf == kNBuf - 1 ? 0 : dbuf + 1;
-                }
-                // units still in flight (a group whose gather ends first)
-                if (prod_wave)
-                    while (produce_step(lds, wave, opaque_v(lane), 0xffff, true, ps, rec) != 0x7fffffff) {
-                    }
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            }
-        }
-
-        // ---- epilogue (k_stream's, HOW 0): park, re-read as rows, store ----
-        __syncthreads();
-        const unsigned long long fst2 = FST_NOW();
-        if (threadIdx.x < 64) FST_ADD(lds, 1, fst2 - fst1);
-        {
-            const int lane = opaque_v(threadIdx.x & 63);
-            const int wave = opaque_s(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
-            const ItemPos q = item_pos(item);
-            const int g = q.cb * kWaves + wave;
-            cFusedArgs* F = fargs();
-            const bool active = g < F->G;
-            const int m0 = q.m0, z = q.z;
-            const int ncols = F->ncols, M = F->M, ldy = F->ldy;
-            const float a = F->a;
-            const float* Bias = F->Bias;
-            float* Y = F->Y;
-            float* ws = F->ws;
-            constexpr int kQ = kCW / 4;
-            constexpr int kStride = kCW * 4 + 16;
-            constexpr int kEpiRows = (kWaves * 128 * kStride <= kFusedStateOff) ? 128 : 64;
-            constexpr int kLanesPerPass = kEpiRows / 4;
-            constexpr int kRowsPerRead = 64 / kQ;
-            char* region = lds + wave * (kEpiRows * kStride);
-            const int col0 = group_col0(g);
-            const int col_end = min(col0 + wave_cols(wave), ncols);
-            const bool vec_ok = OUT == 0 ? ((ldy & 3) == 0 && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0))
-                                         : ((ncols & 3) == 0 && ((reinterpret_cast<uintptr_t>(ws) & 15) == 0));
-            constexpr bool kAddBias = OUT == 0 && !BIAS_FIRST;
-#pragma unroll
-            for (int h = 0; h < 256 / kEpiRows; ++h) {
-                if (active && lane / kLanesPerPass == h) {
-                    const int lh = lane % kLanesPerPass;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int R = 4 * lh + r;
-#pragma unroll
-                        for (int q = 0; q < kQ; ++q) {
-                            const float4 v = make_float4(acc_get(acc, 4 * (4 * q + 0) + r), acc_get(acc, 4 * (4 * q + 1) + r),
-                                                         acc_get(acc, 4 * (4 * q + 2) + r), acc_get(acc, 4 * (4 * q + 3) + r));
-                            *reinterpret_cast<float4*>(region + R * kStride + q * 16) = v;
-                        }
-                    }
-                }
-                __syncthreads();
-                if (active && lane < kRowsPerRead * kQ) {
-                    const int q = lane % kQ;
-                    const int col = col0 + 4 * q;
-                    float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (kAddBias) {
-                        bq.x = col + 0 < col_end ? Bias[col + 0] : 0.f;
-                        bq.y = col + 1 < col_end ? Bias[col + 1] : 0.f;
-                        bq.z = col + 2 < col_end ? Bias[col + 2] : 0.f;
-                        bq.w = col + 3 < col_end ? Bias[col + 3] : 0.f;
-                    }
-#pragma unroll 4
-                    for (int i = 0; i < (kEpiRows + kRowsPerRead - 1) / kRowsPerRead; ++i) {
-                        const int R = lane / kQ + kRowsPerRead * i;
-                        const int row = m0 + kEpiRows * h + R;
-                        if (R >= kEpiRows) break;
-                        float4 v = *reinterpret_cast<const float4*>(region + R * kStride + q * 16);
-                        if (row < M && col < col_end) {
-                            float* dst;
-                            if (OUT == 0) {
-                                dst = Y + (size_t)row * ldy + col;
-                                if (kAddBias) {
-                                    v.x += bq.x;
-                                    v.y += bq.y;
-                                    v.z += bq.z;
-                                    v.w += bq.w;
-                                }
-                                if (PRELU) {
-                                    v.x = (v.x < 0.0f) ? a * v.x : v.x;
-                                    v.y = (v.y < 0.0f) ? a * v.y : v.y;
-                                    v.z = (v.z < 0.0f) ? a * v.z : v.z;
-                                    v.w = (v.w < 0.0f) ? a * v.w : v.w;
-                                }
-                            } else {
-                                dst = ws + ((size_t)z * M + row) * ncols + col;
-                            }
-                            if (vec_ok && col + 3 < col_end) {
-                                if (OUT == 0) {
-                                    typedef float nt4 __attribute__((ext_vector_type(4)));
-                                    nt4 w = {v.x, v.y, v.z, v.w};
-                                    __builtin_nontemporal_store(w, reinterpret_cast<nt4*>(dst));
-                                } else {
-                                    *reinterpret_cast<float4*>(dst) = v;
-                                }
-                            } else {
-                                dst[0] = v.x;
-                                if (col + 1 < col_end) dst[1] = v.y;
-                                if (col + 2 < col_end) dst[2] = v.z;
-                                if (col + 3 < col_end) dst[3] = v.w;
-                            }
-                        }
-                    }
-                }
-                if (h + 1 < 256 / kEpiRows) __syncthreads();
-            }
-        }
-        if (threadIdx.x < 64) FST_ADD(lds, 2, FST_NOW() - fst2);
-    }
-    // the last workgroup to finish advances the epoch (the counter wraps to 0)
-    __syncthreads();
-#if TCSC_FUSED_STAMPS
-    if (threadIdx.x < 16)
-        atomicAdd(&g_fstamp[(blockIdx.x & 4095) * 16 + threadIdx.x],
-                  reinterpret_cast<const unsigned long long*>(lds + kFusedLdsBytes0)[threadIdx.x]);
-#endif
-    if (threadIdx.x == 0) {
-        unsigned* sync = fargs()->sync;
-        const unsigned e = reinterpret_cast<const unsigned*>(lds + kFusedStateOff)[11];
-        if (atomicInc(sync + 1, gridDim.x - 1u) == gridDim.x - 1u)
-            __hip_atomic_store(sync, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -2179,19 +1317,19 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
     if (g.order == 1) {
         hipLaunchKernelGGL((k_stream<BF, PR, 0, 1>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
                            g.n_entries, g.ent2, g.sptr2, g.n_entries2, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy,
-                           g.a, g.ws, pfd, pfl, nullptr);
+                           g.a, g.ws, pfd, pfl, nullptr, 0);
         return hipGetLastError();
     }
     if (g.order == 2) {
         hipLaunchKernelGGL((k_stream<false, PR, 0, 2>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
                            g.n_entries, g.ent2, g.sptr2, g.n_entries2, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy,
-                           g.a, g.ws, pfd, pfl, nullptr);
+                           g.a, g.ws, pfd, pfl, nullptr, 0);
         return hipGetLastError();
     }
     if (slices == 1) {
         hipLaunchKernelGGL((k_stream<BF, PR, 0, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
                            g.n_entries, g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy,
-                           g.a, g.ws, pfd, pfl, nullptr);
+                           g.a, g.ws, pfd, pfl, nullptr, 0);
         return hipGetLastError();
     }
     const long long total = (long long)g.M * g.ncols;
@@ -2204,12 +1342,12 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
                         g.ccnt != nullptr, vec)) {
         hipLaunchKernelGGL((k_stream<BF, PR, 2, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
                            g.n_entries, g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a,
-                           g.ws, pfd, pfl, g.ccnt);
+                           g.ws, pfd, pfl, g.ccnt, g.combine_giveup);
         return hipGetLastError();
     }
     hipLaunchKernelGGL((k_stream<BF, PR, 1, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr, g.n_entries,
                        g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a, g.ws, pfd,
-                       pfl, nullptr);
+                       pfl, nullptr, 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (vec)
@@ -2221,90 +1359,10 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
     return hipGetLastError();
 }
 
-// The fused persistent launch (k_fused) of a whole call: X^T written by the
-// gather's own workgroups, split-K slabs reduced by k_reduce afterwards.
-template <bool BF, bool PR>
-static hipError_t launch_fused_t(const GemmArgs& g, int slices, hipStream_t st) {
-    const int nch = (g.K + kTK - 1) / kTK;
-#if TCSC_FUSED_DIAG_PURE
-    hipLaunchKernelGGL(k_transpose<true>, dim3((g.K + 127) / 128, ldxt_of(g.M) / 64), dim3(256), 0, st, g.X, g.M, g.K,
-                       g.XT, ldxt_of(g.M));
-#endif
-    int cps = (nch + slices - 1) / slices;
-    slices = (nch + cps - 1) / cps;
-    FusedArgs A;
-    A.X = g.X;
-    A.XT = g.XT;
-    A.M = g.M;
-    A.K = g.K;
-    A.ldxt = ldxt_of(g.M);
-    A.ent = g.ent;
-    A.sptr = g.sptr;
-    A.n_entries = g.n_entries;
-    A.G = g.n_groups;
-    A.ncols = g.ncols;
-    A.nch = nch;
-    A.cps = cps;
-    A.Z = slices;
-    A.ncb = (g.n_groups + kWaves - 1) / kWaves;
-    A.n_items = ((g.M + kTM - 1) / kTM) * slices * A.ncb;
-    A.Bias = g.B;
-    A.Y = g.Y;
-    A.ldy = g.ldy;
-    A.a = g.a;
-    A.ws = g.ws;
-    pf_stream_params(g.n_entries, g.n_groups, nch, &A.pf_dist, &A.pf_lines);
-    A.sync = g.fsync;
-    A.sync_n = g.fsync_n;
-    A.pc = cps >= 128 ? 8 : cps >= 32 ? 4 : 2;
-    // pieces produced in an item's prologue: ~16 chunks' worth, so in-loop
-    // production starts 16 chunks ahead of the poll of the piece it feeds
-    A.lead = env_int("TCSC_FUSED_LEAD", (16 + A.pc - 1) / A.pc);
-    const int P = std::min(A.n_items, std::max(1, g.num_cus));
-    if (slices == 1)
-        hipLaunchKernelGGL((k_fused<BF, PR, 0>), dim3(P), dim3(kWaves * 64), 0, st, A);
-    else
-        hipLaunchKernelGGL((k_fused<BF, PR, 1>), dim3(P), dim3(kWaves * 64), 0, st, A);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || slices == 1) return e;
-    const long long total = (long long)g.M * g.ncols;
-    const bool vec = slices <= 16 && g.ncols % 4 == 0 && g.ldy % 4 == 0 &&
-                     ((reinterpret_cast<uintptr_t>(g.Y) | reinterpret_cast<uintptr_t>(g.ws) |
-                       reinterpret_cast<uintptr_t>(g.B)) & 15) == 0;
-    if (vec)
-        hipLaunchKernelGGL((k_reduce4<BF, PR>), dim3(grid_for(total / 4, 256)), dim3(256), 0, st,
-                           reinterpret_cast<const f32x4_t*>(g.ws), slices, g.M, g.ncols, g.B, g.Y, g.ldy, g.a);
-    else
-        hipLaunchKernelGGL((k_reduce<BF, PR>), dim3(grid_for(total, 256)), dim3(256), 0, st, g.ws, slices, g.M,
-                           g.ncols, g.B, g.Y, g.ldy, g.a);
-    return hipGetLastError();
-}
-
-#if TCSC_FUSED_STAMPS
-}  // namespace tcsc
-extern "C" int tcsc_diag_fused_stamps(unsigned long long* out, int n) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tcsc::g_fstamp), (size_t)n * 8) != hipSuccess) return -1;
-    static unsigned long long zero[4096 * 16];
-    return hipMemcpyToSymbol(HIP_SYMBOL(tcsc::g_fstamp), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
-}
-namespace tcsc {
-#endif
-
-bool fused_eligible(const GemmArgs& g) {
-    if (env_int("TCSC_FUSED", 0) == 0) return false;
-    return g.stage == 0 && g.fsync && g.order == 0 && g.num_cus > 0 && g.K >= kTK && g.K % 4 == 0 &&
-           ((reinterpret_cast<uintptr_t>(g.X) & 15) == 0) && (size_t)g.K * 4 * kTM < (1ull << 31);
-}
-
 // g.XT must hold xt_bytes(M, K) (the API layer carves it out of the plan's
 // workspace, ahead of the split-K slabs in g.ws).
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
     if (g.M <= 0 || g.ncols <= 0) return hipSuccess;
-    if (fused_eligible(g)) {
-        const int s = choose_slices(g.M, g.ncols, g.K, g.nnz, g.n_groups, g.ws ? g.ws_bytes : 0, g.force_slices);
-        if (g.bias_first) return g.prelu ? launch_fused_t<true, true>(g, s, st) : launch_fused_t<true, false>(g, s, st);
-        return g.prelu ? launch_fused_t<false, true>(g, s, st) : launch_fused_t<false, false>(g, s, st);
-    }
     if (g.K > 0 && g.stage != 2) {
         if (!g.XT) return hipErrorInvalidValue;
         const int ldxt = ldxt_of(g.M);
@@ -2400,6 +1458,9 @@ int ldxt_for(int M) { return ldxt_of(M); }
 #ifdef TCSC_STAMPS
 extern "C" __attribute__((visibility("default"))) int tcsc_debug_stamps(void* dst, size_t bytes) {
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps), bytes < sizeof(g_stamps) ? bytes : sizeof(g_stamps));
+}
+extern "C" __attribute__((visibility("default"))) int tcsc_debug_wgtimes(void* dst, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_wgtime), bytes < sizeof(g_wgtime) ? bytes : sizeof(g_wgtime));
 }
 #endif
 

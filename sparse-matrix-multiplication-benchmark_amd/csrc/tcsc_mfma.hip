@@ -23,9 +23,9 @@
 // 2^-126 may be flushed.  k_split3 flags every row holding a non-finite x
 // or a nonzero |x| < 2^-100 (it writes every row's flag on every call, so a
 // captured graph replays correctly); k_fixup rewrites those rows from the
-// plan's per-column CSC copy, +1 and -1 rows merged in ascending k (+1 first
-// on a tie), bias first for tcsc_sgemm_basic, then the PReLU -- the exact
-// arithmetic of k_stream's fast order.
+// plan's merged per-column CSC copy, +1 and -1 rows in ascending k (+1 first
+// on a tie), then the bias, then the PReLU -- the exact arithmetic of
+// k_stream's fast order (= the reference's dense.c gemm_basic order).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -151,30 +151,41 @@ __global__ void k_copy_from(const int* __restrict__ src, const int* __restrict__
         dst[i] = src[base + i];
 }
 
+// Merge each column's +1 and -1 rows (rebased lists rp / rn, offsets cp /
+// cn) into one list in ascending row order, the -1 entries tagged with bit
+// 31, a +1 entry first on a tie (k_scatter's rule), at offset cp[j] + cn[j]:
+// the order in which k_stream's fast order adds a column's nonzeros.
+__global__ void k_merge_csc(const int* __restrict__ cp, const int* __restrict__ cn, const int* __restrict__ rp,
+                            const int* __restrict__ rn, int ncols, int* __restrict__ rm) {
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < ncols; j += gridDim.x * blockDim.x) {
+        int p = cp[j], q = cn[j], o = cp[j] + cn[j];
+        const int p1 = cp[j + 1], q1 = cn[j + 1];
+        while (p < p1 || q < q1) {
+            if (q >= q1 || (p < p1 && rp[p] <= rn[q]))
+                rm[o++] = rp[p++];
+            else
+                rm[o++] = (int)((unsigned)rn[q++] | 0x80000000u);
+        }
+    }
+}
+
 // Output (row, j) recomputed exactly as k_stream's fast order (see the file
-// comment): x rebuilt from its three parts, +1 and -1 rows merged in
+// comment): x rebuilt from its three parts, the column's merged rows in
 // ascending k, the bias first or last, then the PReLU.
 template <bool BIAS_FIRST, bool PRELU>
 __device__ inline float exact_out(const uint16_t* __restrict__ X3, int K, int ldk, const int* __restrict__ cp,
-                                  const int* __restrict__ cn, const int* __restrict__ rp,
-                                  const int* __restrict__ rn, const float* __restrict__ Bias, int row, int j,
-                                  float a) {
+                                  const int* __restrict__ cn, const int* __restrict__ rm,
+                                  const float* __restrict__ Bias, int row, int j, float a) {
     const uint16_t* x3 = X3 + (size_t)row * ldk;
     auto xk = [&](int k) {
         return (u2f((uint32_t)x3[x3_index(k, 0)] << 16) + u2f((uint32_t)x3[x3_index(k, 1)] << 16)) +
                u2f((uint32_t)x3[x3_index(k, 2)] << 16);
     };
     float acc = BIAS_FIRST ? Bias[j] : 0.0f;
-    int p = cp[j], q = cn[j];
-    const int p1 = cp[j + 1], q1 = cn[j + 1];
-    while (p < p1 || q < q1) {
-        if (q >= q1 || (p < p1 && rp[p] <= rn[q])) {
-            acc = fmaf(xk(rp[p]), 1.0f, acc);
-            ++p;
-        } else {
-            acc = fmaf(xk(rn[q]), -1.0f, acc);
-            ++q;
-        }
+    const int e1 = cp[j + 1] + cn[j + 1];
+    for (int e = cp[j] + cn[j]; e < e1; ++e) {
+        const int r = rm[e];
+        acc = fmaf(xk(r & 0x7fffffff), r < 0 ? -1.0f : 1.0f, acc);
     }
     if (!BIAS_FIRST) acc += Bias[j];
     if (PRELU) acc = (acc < 0.0f) ? a * acc : acc;
@@ -187,7 +198,7 @@ __device__ inline float exact_out(const uint16_t* __restrict__ X3, int K, int ld
 template <bool BIAS_FIRST, bool PRELU>
 __global__ void __launch_bounds__(256) k_fixup(const uint16_t* __restrict__ X3, int M, int K, int ldk,
                                                const int* __restrict__ cp, const int* __restrict__ cn,
-                                               const int* __restrict__ rp, const int* __restrict__ rn, int ncols,
+                                               const int* __restrict__ rm, int ncols,
                                                const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a,
                                                const int* __restrict__ flags) {
     int any = 0;
@@ -197,7 +208,7 @@ __global__ void __launch_bounds__(256) k_fixup(const uint16_t* __restrict__ X3, 
     if (j >= ncols) return;
     for (int row = 0; row < M; ++row)
         if (flags[row])
-            Y[(size_t)row * ldy + j] = exact_out<BIAS_FIRST, PRELU>(X3, K, ldk, cp, cn, rp, rn, Bias, row, j, a);
+            Y[(size_t)row * ldy + j] = exact_out<BIAS_FIRST, PRELU>(X3, K, ldk, cp, cn, rm, Bias, row, j, a);
 }
 
 // ---------------------------------------------------------------------------
@@ -336,7 +347,8 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
 }  // namespace
 
 hipError_t csc_copy(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int ncols,
-                    long long n_pos, long long n_neg, int* cp, int* cn, int* crp, int* crn, hipStream_t st) {
+                    long long n_pos, long long n_neg, int* cp, int* cn, int* crp, int* crn, int* crm,
+                    hipStream_t st) {
     hipError_t e;
     if ((e = rebase_offsets(csp, col_begin, ncols, cp, st)) != hipSuccess) return e;
     if ((e = rebase_offsets(csn, col_begin, ncols, cn, st)) != hipSuccess) return e;
@@ -344,6 +356,9 @@ hipError_t csc_copy(const int* csp, const int* csn, const int* rip, const int* r
         hipLaunchKernelGGL(k_copy_from, dim3(grid_of(n_pos, 256)), dim3(256), 0, st, rip, csp, col_begin, n_pos, crp);
     if (n_neg > 0)
         hipLaunchKernelGGL(k_copy_from, dim3(grid_of(n_neg, 256)), dim3(256), 0, st, rin, csn, col_begin, n_neg, crn);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (ncols > 0 && n_pos + n_neg > 0)
+        hipLaunchKernelGGL(k_merge_csc, dim3(grid_of(ncols, 256)), dim3(256), 0, st, cp, cn, crp, crn, ncols, crm);
     return hipGetLastError();
 }
 
@@ -398,11 +413,11 @@ hipError_t mfma_gemm3(const uint16_t* x3, const uint16_t* w3, int ldk, int M, in
                  : launch_gemm3_t<false>(x3, w3, ldk, M, N, B, Y, ldy, a, st);
 }
 
-hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cp, const int* cn, const int* crp,
-                      const int* crn, int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu,
-                      float a, const int* flags, hipStream_t st) {
+hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cp, const int* cn, const int* crm,
+                      int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
+                      const int* flags, hipStream_t st) {
     const dim3 grid((ncols + 255) / 256), block(256);
-#define TCSC_FIX_ARGS x3, M, K, ldk, cp, cn, crp, crn, ncols, B, Y, ldy, a, flags
+#define TCSC_FIX_ARGS x3, M, K, ldk, cp, cn, crm, ncols, B, Y, ldy, a, flags
     if (bias_first) {
         if (prelu)
             hipLaunchKernelGGL((k_fixup<true, true>), grid, block, 0, st, TCSC_FIX_ARGS);

@@ -448,8 +448,9 @@ class Plan:
         return {k: getattr(inf, k) for k, _ in plan_info_t._fields_}
 
     def launch_info(self, M: int) -> tuple[str, int]:
-        """(path, K slices) of a launch of M rows: path is 'fused' (k_fused), 'gather'
-        (k_transpose + k_stream), 'mfma' or 'small' (include/tcsc_gpu.h tcsc_gpu_launch_info)."""
+        """(path, K slices) of a launch of M rows: path is 'gather' (k_transpose +
+        k_stream), 'mfma' or 'small' (include/tcsc_gpu.h tcsc_gpu_launch_info; value 1,
+        the retired persistent k_fused, is never returned)."""
         path, slices = C.c_int(), C.c_int()
         _check(lib().tcsc_gpu_launch_info(self.handle, int(M), C.byref(path), C.byref(slices)),
                "tcsc_gpu_launch_info")

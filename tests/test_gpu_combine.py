@@ -165,3 +165,39 @@ def test_launch_combine_reports_the_path(gpu, monkeypatch, M, K, N, density, env
     assert path == "gather" and slices > 1
     assert plan.launch_combine(M) == expect
     plan.destroy()
+
+
+@pytest.mark.parametrize("M,K,N,density,variant,slices", [
+    (1024, 4096, 4096, 0.05, "prelu_basic", None),      # cfg 3: 4 slices
+    (513, 2400, 700, 0.1, "basic", "3"),                # uneven bands
+    (1024, 16384, 1024, 0.02, "prelu_separate", "16"),  # 16 slices: one workgroup reduces all 16 bands
+    (4096, 16384, 2048, 0.02, "prelu_basic", "2"),      # the 8-way column block
+])
+def test_combine_give_up_path_bit_identical(gpu, monkeypatch, M, K, N, density, variant, slices):
+    """the path a slice takes when its partners are not resident
+    (its bounded wait runs out) never ran in a test.  TCSC_COMBINE_GIVEUP=1
+    makes every slice but each tile's last arrival give up at once, so the
+    last arrival claims and reduces every band: the output must still equal
+    the k_reduce4 launch bit for bit, launch after launch on one plan."""
+    import torch
+
+    if slices:
+        monkeypatch.setenv("TCSC_SLICES", slices)
+    plan, _ = _plan(torch, K, N, density, 31 + M)
+    plan.reserve(M)
+    assert plan.launch_combine(M) or slices == "2"
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(77 + K)
+    B = torch.rand((N,), generator=g, device=dev) * 2 - 1
+    for it in range(3):
+        X = torch.rand((M, K), generator=g, device=dev) * 2 - 1
+        monkeypatch.setenv("TCSC_COMBINE_GIVEUP", "1")
+        Yg = _run(torch, plan, X, B, M, N, variant, True, monkeypatch)
+        monkeypatch.delenv("TCSC_COMBINE_GIVEUP")
+        Yc = _run(torch, plan, X, B, M, N, variant, True, monkeypatch)  # the words are back at zero
+        Yr = _run(torch, plan, X, B, M, N, variant, False, monkeypatch)
+        assert not torch.isnan(Yg).any(), f"iteration {it}: bands left unreduced"
+        assert torch.equal(Yg.view(torch.int32), Yr.view(torch.int32)), f"iteration {it}: give-up path"
+        assert torch.equal(Yc.view(torch.int32), Yr.view(torch.int32)), f"iteration {it}: after the give-up path"
+    plan.destroy()

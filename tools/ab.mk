@@ -100,32 +100,9 @@ lib/abl/libtcsc_amd_pfs%.so: $(SRC)/tcsc_kernels.hip $(SRC)/tcsc_api.cpp $(OBJ)/
 	$(HIPCC) $(HIPFLAGS) -DTCSC_PF_S=$* -c $(SRC)/tcsc_api.cpp -o $(OBJ)/abl/a_pfs$*.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)/abl/k_pfs$*.o $(OBJ)/abl/a_pfs$*.o $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o -lpthread -L$(ROCM)/lib -lrocblas -Wl,-rpath,$(ROCM)/lib
 
-# k_fused timing variants (DESIGN.md §4 k_fused; nl gives wrong results, the others are
-# correct): lib/abl/libtcsc_amd_f<v>.so with v =
-#   nl  no in-loop production or polls (timing only)   pu  k_transpose + the gather, no production
-#   st  s_memtime stamps (tools/fused_stamps.py)        rr  round-robin item order
-#   late / prio / lp  producer steps after the gather / at raised priority / both
-#   2w  two producer waves, several stages per step (the first layout)   1a  two waves, one stage
-#   3w  three waves, several stages (the default: 4 k x 256 m units, 3 waves, one stage per step)
-#   small  1 k x 64 m units, 12 waves, one stage per step   sm0  the same, several stages per step
-FDEF_nl := -DTCSC_FUSED_DIAG_NOLOOP=1
-FDEF_pu := -DTCSC_FUSED_DIAG_PURE=1
-FDEF_st := -DTCSC_FUSED_STAMPS=1
-FDEF_rr := -DTCSC_FUSED_XCD_RANGES=0
-FDEF_late := -DTCSC_FUSED_PROD_LATE=1
-FDEF_prio := -DTCSC_FUSED_PROD_PRIO=1
-FDEF_lp := -DTCSC_FUSED_PROD_LATE=1 -DTCSC_FUSED_PROD_PRIO=1
-FDEF_2w := -DTCSC_FUSED_PROD_WAVES=2 -DTCSC_FUSED_ONE_ACTION=0
-FDEF_1a := -DTCSC_FUSED_PROD_WAVES=2 -DTCSC_FUSED_ONE_ACTION=1
-FDEF_3w := -DTCSC_FUSED_PROD_WAVES=3 -DTCSC_FUSED_ONE_ACTION=0
-FDEF_small := -DTCSC_FUSED_SMALL=1
-FDEF_sm0 := -DTCSC_FUSED_SMALL=1 -DTCSC_FUSED_ONE_ACTION=0
-FDEF_skip := -DTCSC_FUSED_PF_SKIP=1
-lib/abl/libtcsc_amd_f%.so: $(SRC)/tcsc_kernels.hip $(SRC)/tcsc_api.cpp $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o $(HDRS) $(SRC)/gather_asm.inc
-	@mkdir -p lib/abl $(OBJ)/abl
-	$(HIPCC) $(HIPFLAGS) $(FDEF_$*) -c $(SRC)/tcsc_kernels.hip -o $(OBJ)/abl/k_f$*.o
-	$(HIPCC) $(HIPFLAGS) $(FDEF_$*) -c $(SRC)/tcsc_api.cpp -o $(OBJ)/abl/a_f$*.o
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)/abl/k_f$*.o $(OBJ)/abl/a_f$*.o $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o -lpthread -L$(ROCM)/lib -lrocblas -Wl,-rpath,$(ROCM)/lib
+# k_fused (the persistent gather with in-kernel X^T production, round 4) left the
+# library in round 5: the kernel, its launcher and its A/B variants are at commit
+# 815156e (csrc/tcsc_kernels.hip k_fused, tools/ab.mk lib/abl/libtcsc_amd_f<v>.so).
 
 # 4-byte entry cost proxy: the generated loop rebuilds the +-1
 # multiplier from a sign bit with 2 SALU per entry (gen_gather_asm.py --sgn 1);
