@@ -218,9 +218,9 @@ def main():
     plan.prepare_x(X, cfg.M, sh)
     gather_s = timed(lambda: plan.sgemm_prepared(B, Y, cfg.M, ncols, variant, 0.2, sh), nsplit)
     kernel_s = gather_s
-    combine = plan.launch_combine(cfg.M) if slices > 1 else False
-    kernel_name = "k_stream" + ((" (+ in-launch combine)" if combine else " + k_reduce4") + f", {slices} K slices"
-                                if slices > 1 else "")
+    combine = plan.combine_mode(cfg.M) if slices > 1 else None
+    kernel_name = "k_stream" + ((f" (+ in-launch {combine} combine)" if combine else " + k_reduce4") +
+                                f", {slices} K slices" if slices > 1 else "")
 
     alt = None
     if distributed and args.scaling == "strong" and not args.no_alt_shard and args.shard_of <= 1:
@@ -493,7 +493,8 @@ def other_configs(args, tcsc_amd, workloads, dev, sh, timed, skip):
         mfma = lpath == "mfma"
         path = {"mfma": "mfma (bf16 x3 split GEMM: k_split3 + k_gemm3)", "small": "small-M (one wave per column)",
                 "gather": "gather (k_transpose + k_stream)"}[lpath] + \
-            ((f", K split {lslices} ways, combined in the k_stream launch" if plan.launch_combine(c.M) else
+            ((f", K split {lslices} ways, combined in the k_stream launch ({plan.combine_mode(c.M)})"
+              if plan.launch_combine(c.M) else
               f", K split {lslices} ways + k_reduce4") if lslices > 1 else "")
         r = {
             "workload": c.describe(), "variant": c.variant, "nnz": nnz, "ms": t * 1e3,

@@ -125,12 +125,16 @@ enum tcsc_path {
 };
 int tcsc_gpu_launch_info(const tcsc_gpu_plan *plan, int M, int *path, int *slices);
 
-/* For TCSC_PATH_GATHER with a K split: *in_launch = 1 when the split-K slabs
- * are combined inside the k_stream launch (the grid fits the chip at one
- * workgroup per CU, >= 3 slices, >= 64 workgroups, N % 4 == 0, the plan's
- * reserved workspace; TCSC_COMBINE=0/1 overrides the slice and size rule),
- * 0 when k_reduce runs after it or nothing is split.  Y and bias are assumed
- * 16-B aligned with ldy = N; otherwise the launch uses k_reduce. */
+/* For TCSC_PATH_GATHER with a K split, where the split-K slabs are combined
+ * (N % 4 == 0 and the plan's reserved workspace needed for either in-launch
+ * form; TCSC_COMBINE=0 turns both off, =1 lifts the band form's size rule):
+ *   3  inside the k_stream launch, pairwise (exactly 2 slices: the tile's
+ *      first slice to finish stores its slab, the second combines; any grid)
+ *   2  inside the k_stream launch, by row bands (>= 3 slices, the grid fits
+ *      the chip at one workgroup per CU, >= 64 workgroups)
+ *   0  by k_reduce after it, or nothing is split.
+ * Y and bias are assumed 16-B aligned with ldy = N; otherwise the launch
+ * uses k_reduce. */
 int tcsc_gpu_launch_combine(const tcsc_gpu_plan *plan, int M, int *in_launch);
 
 /* Allocate the plan's workspace for launches of up to `max_M` rows: X^T

@@ -899,10 +899,8 @@ int tcsc_gpu_launch_combine(const tcsc_gpu_plan* p, int M, int* in_launch) {
     const int s = tcsc::normalized_slices(p->rows, slices);
     const long long cb = (p->n_groups + tcsc::kWaves - 1) / tcsc::kWaves, rt = (rows + tcsc::kTM - 1) / tcsc::kTM;
     const bool words = p->csync != nullptr;
-    *in_launch = tcsc::combine_applies(s, cb * rt * s, cb * rt, (long long)rows * p->cols, words ? p->num_cus : 0,
-                                       words, p->cols % 4 == 0)
-                     ? 1
-                     : 0;
+    *in_launch = tcsc::combine_mode(s, cb * rt * s, cb * rt, (long long)rows * p->cols, words ? p->num_cus : 0, words,
+                                    p->cols % 4 == 0);
     return TCSC_OK;
 }
 

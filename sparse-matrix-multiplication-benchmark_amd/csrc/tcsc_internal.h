@@ -168,7 +168,7 @@ struct PlanOut {
 // tile's last workgroup to finish, so every launch (and graph replay) finds
 // them at zero.  A launch that returns an error marks the block dirty and
 // the next launch on the plan re-zeroes it first (tcsc_api.cpp).
-constexpr int kCombineTiles = 256;
+constexpr int kCombineTiles = 4096;
 constexpr int kCombineWords = 32;  // per tile: 2 + Z (Z <= 16) used
 constexpr size_t kCombineBytes = (size_t)kCombineTiles * kCombineWords * 4;
 
@@ -209,9 +209,11 @@ hipError_t plan_counts(const PlanDev& in, PlanOut& out, hipStream_t st);    // -
 hipError_t plan_fill(const PlanDev& in, PlanOut& out, hipStream_t st);      // -> sptr, ent
 // Launch
 int choose_slices(int M, int ncols, int K, long long nnz, int n_groups, size_t ws_bytes, int force);
-// the split-K combine of a gather launch runs inside k_stream (combine_tile)
-bool combine_applies(int slices, long long wgs, long long tiles, long long slab_floats, int num_cus, bool have_words,
-                     bool vec);
+// where the split-K slabs of a gather launch are combined: 0 by k_reduce4
+// after it, 2 inside k_stream by row bands (combine_tile: >= 3 slices, the
+// grid resident at once), 3 inside k_stream pairwise (exactly 2 slices)
+int combine_mode(int slices, long long wgs, long long tiles, long long slab_floats, int num_cus, bool have_words,
+                 bool vec);
 int normalized_slices(int K, int slices);  // the K split launch_gemm actually runs
 // stream prefetch of a plan of n_entries entries over n_groups x n_chunks
 // streams: *dist bytes ahead, *lines 128-B lines (TCSC_PF_DIST / TCSC_PF_LINES override)

@@ -638,6 +638,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
          const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a, float* __restrict__ ws, int pf_dist,
          int pf_lines, unsigned* __restrict__ ccnt, int combine_giveup) {
     static_assert(ORDER == 0 || OUT == 0, "the reference orders do not split K");
+    static_assert(OUT >= 0 && OUT <= 3, "OUT: 0 Y, 1 slab, 2 slab + band combine, 3 pairwise combine (2 slices)");
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -797,9 +798,37 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     // after the +1 chain) acc + bias parked in Y as is; 2 (order 2, after the
     // -1 chain) the parked value + acc, then PReLU.  A thread re-reads in
     // HOW 2 exactly the elements it stored in HOW 1.
+    // OUT 3 (split-K over exactly 2 slices, DESIGN.md §4 k_reduce "pairwise"):
+    // the tile's first slice to finish its chunk loop (its add to the
+    // arrival word returns 0) stores its partial slab (sc1) and then adds 1
+    // to the tile's ready word; the second polls the ready word, re-zeroes
+    // both words, and writes Y = act((0 + s0) + s1 + b) from its registers
+    // and the partner's slab, in slice order -- k_reduce4's adds, the same
+    // bits.  The first finisher never waits, so no residency is assumed.
+    int pair_role = 0;  // OUT 3: 0 = store the slab, 1 = combine
+    unsigned* const pw = OUT == 3 ? ccnt + (size_t)(t.rt * (int)gridDim.x + t.cb) * kCombineWords : nullptr;
     auto epilogue = [&](auto how_) {
         constexpr int HOW = decltype(how_)::value;
         __syncthreads();  // every wave is done with the tile ring
+        if constexpr (OUT == 3) {
+            int* role = reinterpret_cast<int*>(lds + kLdsBytes - 16);
+            if (threadIdx.x == 0) {
+                int r = __hip_atomic_fetch_add(pw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u ? 0 : 1;
+                if (r == 1) {
+                    // the partner has arrived, so it is running and will publish: the bound
+                    // (100 ms) only keeps a broken launch from hanging the device
+                    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                    while (__hip_atomic_load(pw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+                           __builtin_amdgcn_s_memrealtime() - t0 < 10000000ull)
+                        __builtin_amdgcn_s_sleep(2);
+                    __hip_atomic_store(pw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(pw + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                role[0] = r;
+            }
+            __syncthreads();
+            pair_role = __builtin_amdgcn_readfirstlane(role[0]);
+        }
         constexpr int kQ = kCW / 4;                 // 16-B quads per row
         constexpr int kStride = kCW * 4 + 16;       // bytes per parked row
         constexpr int kEpiRows = (kWaves * 128 * kStride <= kLdsBytes) ? 128 : 64;
@@ -814,6 +843,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         const __amdgpu_buffer_rsrc_t slab_rs = slabs_rsrc(ws, (int)gridDim.z, M, ncols);
         constexpr bool kAddBias = OUT == 0 && (HOW == 1 || (HOW == 0 && !BIAS_FIRST));
         constexpr bool kPrelu = PRELU && HOW != 1;
+        constexpr bool kLoadBias = kAddBias || OUT == 3;
 #pragma unroll
         for (int h = 0; h < 256 / kEpiRows; ++h) {
             if (active && lane / kLanesPerPass == h) {
@@ -835,7 +865,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                 const int q = lane % kQ;
                 const int col = col0 + 4 * q;
                 float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (kAddBias) {
+                if (kLoadBias) {
                     bq.x = col + 0 < col_end ? Bias[col + 0] : 0.f;
                     bq.y = col + 1 < col_end ? Bias[col + 1] : 0.f;
                     bq.z = col + 2 < col_end ? Bias[col + 2] : 0.f;
@@ -873,7 +903,43 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                         } else {
                             dst = ws + ((size_t)t.z * M + row) * ncols + col;
                         }
-                        if constexpr (OUT == 2) {
+                        if constexpr (OUT == 3) {
+                            // vec_ok and whole quads (the launcher's conditions)
+                            const int off = (int)(((size_t)t.z * M + row) * ncols + col) * 4;
+                            if (pair_role == 0) {
+                                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), slab_rs, off, 0,
+                                                                       kSc1);
+                            } else {
+                                const int poff = (int)(((size_t)(1 - t.z) * M + row) * ncols + col) * 4;
+                                const float4 pv = __builtin_bit_cast(
+                                    float4, __builtin_amdgcn_raw_buffer_load_b128(slab_rs, poff, 0, kSc1));
+                                const float4 lo = t.z == 0 ? v : pv, hi = t.z == 0 ? pv : v;
+                                float4 o = BIAS_FIRST ? bq : make_float4(0.f, 0.f, 0.f, 0.f);
+                                o.x += lo.x;
+                                o.y += lo.y;
+                                o.z += lo.z;
+                                o.w += lo.w;
+                                o.x += hi.x;
+                                o.y += hi.y;
+                                o.z += hi.z;
+                                o.w += hi.w;
+                                if (!BIAS_FIRST) {
+                                    o.x += bq.x;
+                                    o.y += bq.y;
+                                    o.z += bq.z;
+                                    o.w += bq.w;
+                                }
+                                if (PRELU) {
+                                    o.x = (o.x < 0.0f) ? a * o.x : o.x;
+                                    o.y = (o.y < 0.0f) ? a * o.y : o.y;
+                                    o.z = (o.z < 0.0f) ? a * o.z : o.z;
+                                    o.w = (o.w < 0.0f) ? a * o.w : o.w;
+                                }
+                                typedef float nt4 __attribute__((ext_vector_type(4)));
+                                nt4 w = {o.x, o.y, o.z, o.w};
+                                __builtin_nontemporal_store(w, reinterpret_cast<nt4*>(Y + (size_t)row * ldy + col));
+                            }
+                        } else if constexpr (OUT == 2) {
                             // write-through (sc1) slab stores: the tile's other
                             // workgroups read them with sc1 loads (combine_tile)
                             const int off = (int)(((size_t)t.z * M + row) * ncols + col) * 4;
@@ -921,6 +987,13 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         rt_[3] = rtstamp();
 #endif
         if constexpr (OUT == 2) combine_tile<BIAS_FIRST, PRELU>(ws, M, ncols, Bias, Y, ldy, a, ccnt, t, lds, combine_giveup);
+        if constexpr (OUT == 3) {
+            if (pair_role == 0) {  // publish the slab: every wave's sc1 stores drained, then one agent add
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (threadIdx.x == 0) __hip_atomic_fetch_add(pw + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
 #ifdef TCSC_STAMPS
         rt_[4] = rtstamp();
         if (threadIdx.x == 0) {
@@ -1280,20 +1353,26 @@ void pf_stream_params(long long n_entries, int n_groups, int n_chunks, int* dist
     *lines = l;
 }
 
-// Split-K slabs combined inside the k_stream launch (combine_tile) where the
-// grid is resident at once, or by k_reduce4 after it.  TCSC_COMBINE unset:
-// in-launch from 3 slices and 64 workgroups on (measured: cfg 2/3 at 4
-// slices 79 -> 74 us; the 8-way cfg 4 block at 2 slices 0.186 -> 0.192 ms, a
-// tile's two slices wait on each other longer than the reduce launch takes;
-// cfg 1's 6 workgroups 23 -> 27 us, the hand-off's atomics in series cost
-// more than a launch); 1: wherever it applies; 0: never.
-bool combine_applies(int slices, long long wgs, long long tiles, long long slab_floats, int num_cus, bool have_words,
-                     bool vec) {
-    if (slices < 2 || slices > 16 || !vec || !have_words || num_cus <= 0 || wgs > num_cus || tiles > kCombineTiles ||
+// Split-K slabs combined inside the k_stream launch or by k_reduce4 after it.
+//  * 2 slices: pairwise (k_stream OUT 3): the tile's first slice to finish
+//    stores its slab, the second combines -- no reduce launch, half the slab
+//    bytes, and no wait on a workgroup that has not started, so any grid.
+//  * 3 or more: row bands (combine_tile, OUT 2) where the whole grid is
+//    resident (one workgroup per CU), from 64 workgroups on (measured: cfg
+//    2/3 at 4 slices 79 -> 74 us; cfg 1's 6 workgroups 23 -> 27 us: the
+//    hand-off's atomics in series cost more than a launch).
+// TCSC_COMBINE unset: that policy; 1: in-launch wherever it can run; 0: never;
+// 2: row bands wherever the grid is resident, 2 slices included (A/B).
+int combine_mode(int slices, long long wgs, long long tiles, long long slab_floats, int num_cus, bool have_words,
+                 bool vec) {
+    if (slices < 2 || slices > 16 || !vec || !have_words || tiles > kCombineTiles ||
         slab_floats * slices * 4 >= 0x7fffffffLL)
-        return false;
+        return 0;
     const int c = env_int("TCSC_COMBINE", -1);
-    return c < 0 ? (slices >= 3 && wgs >= 64) : c != 0;
+    if (c == 0) return 0;
+    if (slices == 2 && (c != 2 || num_cus <= 0 || wgs > num_cus)) return 3;
+    if (num_cus <= 0 || wgs > num_cus) return 0;
+    return (c > 0 || wgs >= 64) ? 2 : 0;
 }
 
 int normalized_slices(int K, int slices) {
@@ -1336,10 +1415,15 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
     const bool vec = slices <= 16 && g.ncols % 4 == 0 && g.ldy % 4 == 0 &&
                      ((reinterpret_cast<uintptr_t>(g.Y) | reinterpret_cast<uintptr_t>(g.ws) |
                        reinterpret_cast<uintptr_t>(g.B)) & 15) == 0;
-    // the in-launch combine (combine_tile): every workgroup of the grid
-    // resident at once (one per CU), so a tile's slices can wait for each other
-    if (combine_applies(slices, (long long)grid.x * grid.y * grid.z, (long long)grid.x * grid.y, total, g.num_cus,
-                        g.ccnt != nullptr, vec)) {
+    const int cm = combine_mode(slices, (long long)grid.x * grid.y * grid.z, (long long)grid.x * grid.y, total,
+                                g.num_cus, g.ccnt != nullptr, vec);
+    if (cm == 3) {  // pairwise: no residency needed
+        hipLaunchKernelGGL((k_stream<BF, PR, 3, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
+                           g.n_entries, g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a,
+                           g.ws, pfd, pfl, g.ccnt, 0);
+        return hipGetLastError();
+    }
+    if (cm == 2) {  // row bands: every workgroup of the grid resident at once (one per CU)
         hipLaunchKernelGGL((k_stream<BF, PR, 2, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
                            g.n_entries, g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a,
                            g.ws, pfd, pfl, g.ccnt, g.combine_giveup);

@@ -127,17 +127,19 @@ def test_shape_rules_fail_loudly(gpu, monkeypatch):
 def test_bcsr_1x8_equals_tcsc_basic(gpu, torch_cuda, oracle, monkeypatch):
     """Ternary W with 1x8 blocks: bcsr_sgemm_basic adds bias first, then
     X[m,k]*w for every k of a stored block in ascending k -- zeros add +-0,
-    an exact no-op here -- which is the TCSC kernel's basic order (bias
-    first, +1/-1 merged in ascending k) when K is not split over workgroups
+    an exact no-op here -- which is the TCSC kernel's fast order (+1/-1
+    merged in ascending k) when K is not split over workgroups
     (TCSC_SLICES=1; this grid is small enough for the cost model to split
-    it).  Bit-identical outputs."""
+    it), except where the bias goes: the TCSC fast order adds it after the
+    sum (dense.c's gemm_basic order).  With a zero bias the
+    two orders are the same arithmetic: bit-identical outputs."""
     monkeypatch.setenv("TCSC_SLICES", "1")
     torch = torch_cuda
     dev = torch.device("cuda:0")
     M, K, N = 700, 2048, 1032
     X = oracle.uniform((M, K), 81)
     Wd = oracle.ternary((K, N), 0.02, 82)
-    B = oracle.uniform((N,), 83)
+    B = np.zeros((N,), np.float32)
     Wb = bcsr.BcsrMatrix.from_dense(Wd, 1, 8)
     Wt = tcsc_amd.TcscMatrix.from_dense(Wd)
     st = torch.cuda.current_stream().cuda_stream
@@ -156,8 +158,9 @@ def test_bcsr_1x8_equals_tcsc_basic(gpu, torch_cuda, oracle, monkeypatch):
 
 def test_baseline_cfg4_shape_1x8(gpu, torch_cuda, oracle, monkeypatch):
     """BASELINE cfg4 (M=4096, K=N=16384, 98 % ternary) as 1x8 BCSR: whole
-    output bit-identical to the TCSC kernel's basic result, sampled rows
-    bit-identical to the oracle (bcsr_sgemm_basic and prelu_basic order)."""
+    output bit-identical to the TCSC kernel's basic result on a zero bias
+    (where bias-first BCSR and the bias-last TCSC fast order agree), sampled
+    rows bit-identical to the oracle (bcsr_sgemm_basic and prelu_basic order)."""
     monkeypatch.setenv("TCSC_SLICES", "1")
     torch = torch_cuda
     cfg = workloads.CONFIGS[4]
@@ -175,10 +178,13 @@ def test_baseline_cfg4_shape_1x8(gpu, torch_cuda, oracle, monkeypatch):
     del Wd
     pt = tcsc_amd.Plan(Wt, 0, N, 0, st)
     Yt = torch.empty((M, N), device=dev)
-    pt.sgemm(X, B, Yt, M, N, "basic", 0.0, st)
+    Z = torch.zeros_like(B)  # bias first (BCSR) and last (TCSC fast order) agree on a zero bias
+    pt.sgemm(X, Z, Yt, M, N, "basic", 0.0, st)
+    Yz = torch.empty_like(Yb)
+    pb.sgemm(X, Z, Yz, M, N, K, N, "basic", 0.0, st)
     torch.cuda.synchronize()
-    assert torch.equal(Yb, Yt)
-    del Yt
+    assert torch.equal(Yz, Yt)
+    del Yt, Yz
     pt.destroy()
     Wt.free()
     rows = np.array([0, 1, 1234, M - 1])

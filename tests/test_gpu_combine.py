@@ -1,5 +1,6 @@
-"""The in-launch split-K combine (k_stream OUT 2, `combine_tile`, DESIGN.md
-§4 k_reduce; TCSC_COMBINE=1) against the k_stream + k_reduce4 pair
+"""The in-launch split-K combines (k_stream OUT 2, `combine_tile`, by row
+bands; OUT 3, pairwise, at 2 slices; DESIGN.md §4 k_reduce; TCSC_COMBINE=1)
+against the k_stream + k_reduce4 pair
 (TCSC_COMBINE=0): the same adds in the same order per element, so the outputs
 must be bit-identical -- on cfg 2/3, on ragged shapes (M not a multiple of
 256, the last column block partial), for forced slice counts 2, 3 (uneven row
@@ -144,11 +145,12 @@ def test_combine_graph_replay_with_new_x(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("M,K,N,density,env,expect", [
-    (1024, 4096, 4096, 0.05, None, True),      # cfg 2: 4 slices, 256 workgroups
-    (1024, 4096, 4096, 0.05, "0", False),      # switched off
-    (128, 256, 256, 0.1, None, False),         # cfg 1: 6 workgroups, k_reduce4 is cheaper
-    (128, 256, 256, 0.1, "1", True),           # forced
-    (2048, 4096, 8192, 0.05, "1", False),      # 2 slices x 256 tiles: the grid exceeds the chip
+    (1024, 4096, 4096, 0.05, None, "bands"),      # cfg 2: 4 slices, 256 workgroups
+    (1024, 4096, 4096, 0.05, "0", None),          # switched off
+    (128, 256, 256, 0.1, None, None),             # cfg 1: 6 workgroups, k_reduce4 is cheaper
+    (128, 256, 256, 0.1, "1", "bands"),           # forced
+    (2048, 4096, 8192, 0.05, None, "pairwise"),   # 2 slices x 256 tiles: the grid exceeds the chip, pairs need no residency
+    (2048, 4096, 8192, 0.05, "0", None),
 ])
 def test_launch_combine_reports_the_path(gpu, monkeypatch, M, K, N, density, env, expect):
     import torch
@@ -163,7 +165,8 @@ def test_launch_combine_reports_the_path(gpu, monkeypatch, M, K, N, density, env
     plan.reserve(M)
     path, slices = plan.launch_info(M)
     assert path == "gather" and slices > 1
-    assert plan.launch_combine(M) == expect
+    assert plan.combine_mode(M) == expect
+    assert plan.launch_combine(M) == (expect is not None)
     plan.destroy()
 
 
@@ -185,7 +188,8 @@ def test_combine_give_up_path_bit_identical(gpu, monkeypatch, M, K, N, density, 
         monkeypatch.setenv("TCSC_SLICES", slices)
     plan, _ = _plan(torch, K, N, density, 31 + M)
     plan.reserve(M)
-    assert plan.launch_combine(M) or slices == "2"
+    monkeypatch.setenv("TCSC_COMBINE", "1")
+    assert plan.combine_mode(M) == ("pairwise" if slices == "2" else "bands")
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)
     g.manual_seed(77 + K)

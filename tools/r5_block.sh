@@ -26,4 +26,13 @@ if [ "${PROF:-1}" = 1 ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof8 -o run -- python bench.py --shard-of 8 --shard cols --steps 10 --warmup 2 $F > $OUT/prof8.log 2>&1 || { tail $OUT/prof8.log; exit 1; }
   python tools/prof_summary.py $OUT/prof8/run_kernel_trace.csv 10 > $OUT/prof8_summary.json 2>&1; head -c 1500 $OUT/prof8_summary.json
 fi
+if [ "${PMC:-1}" = 1 ]; then
+  # HBM traffic (FETCH_SIZE, WRITE_SIZE, TCC hit/miss, FETCH_SIZE of the no-DMA build) and
+  # one SQ pass, each its own rocprofv3 run, of the 8-way block's k_stream (2 K slices: the
+  # slab-writing instantiation OUT 1) -> TRAFFIC_KEY cfg4:prelu_basic:2048 (tools/traffic_json.py)
+  BENCH_ARGS="--shard-of 8 --no-other-configs --no-reference-order --no-bcsr --no-dense-baseline" \
+    TRAFFIC_DIR=gpurun_out/tr8_ ABL_LIB=$PWD/sparse-matrix-multiplication-benchmark_amd/lib/diag/libtcsc_amd_abl0_nd.so \
+    bash tools/traffic.sh || exit 1
+  BENCH_ARGS="--shard-of 8" SQ_DIR=gpurun_out/sq8 bash tools/sq_pass.sh || exit 1
+fi
 echo ALL_DONE

@@ -3,9 +3,10 @@
 # only, no sys/runtime trace): where k_stream's wave-cycles go (issuing,
 # waiting on s_waitcnt / barrier, issue stalls) and how busy the LDS is.
 cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp; mkdir -p gpurun_out
-rm -rf gpurun_out/sq
+D=${SQ_DIR:-gpurun_out/sq}
+rm -rf $D
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
-    SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES --output-format csv -d gpurun_out/sq -o run -- \
+    SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES --output-format csv -d $D -o run -- \
     python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-dense-baseline --no-bcsr --no-host-api --no-graph \
-    --no-other-configs --no-reference-order ${BENCH_ARGS:-} > gpurun_out/sq.log 2>&1
+    --no-other-configs --no-reference-order ${BENCH_ARGS:-} > $D.log 2>&1
 echo "sq pass rc=$?"

@@ -43,12 +43,13 @@ def per_dispatch(root, counter, kernel=KERNEL):
 
 
 def main():
-    out = os.path.join(ROOT, "gpurun_out")
-    fetch = per_dispatch(os.path.join(out, "traffic1"), "FETCH_SIZE")
-    write = per_dispatch(os.path.join(out, "traffic2"), "WRITE_SIZE")
-    nodma = per_dispatch(os.path.join(out, "traffic4"), "FETCH_SIZE")
-    hit = per_dispatch(os.path.join(out, "traffic3"), "TCC_HIT_sum")
-    miss = per_dispatch(os.path.join(out, "traffic3"), "TCC_MISS_sum")
+    # TRAFFIC_DIR: the passes' directory prefix (tools/traffic.sh), default gpurun_out/traffic
+    pre = os.path.join(ROOT, os.environ.get("TRAFFIC_DIR", "gpurun_out/traffic"))
+    fetch = per_dispatch(pre + "1", "FETCH_SIZE")
+    write = per_dispatch(pre + "2", "WRITE_SIZE")
+    nodma = per_dispatch(pre + "4", "FETCH_SIZE")
+    hit = per_dispatch(pre + "3", "TCC_HIT_sum")
+    miss = per_dispatch(pre + "3", "TCC_MISS_sum")
     if not fetch or not write:
         print("no k_stream dispatches found", file=sys.stderr)
         return 1
