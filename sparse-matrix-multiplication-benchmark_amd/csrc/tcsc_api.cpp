@@ -68,8 +68,9 @@ struct tcsc_gpu_plan {
     size_t mfma_bytes = 0;
     // the column range's rebased CSC (fast-order plans): the small-M path
     // walks it, the MFMA path's fixup recomputes flagged rows from it
-    // (crm: each column's +1 / -1 rows merged in ascending k, -1 tagged in bit 31)
-    int *ccp = nullptr, *ccn = nullptr, *crm = nullptr;
+    // (crq: each column's +1 / -1 rows merged in ascending k, in the quad
+    // layout of 64-column groups whose quad offsets are ccq: tcsc_internal.h)
+    int *ccq = nullptr, *crq = nullptr;
     size_t csc_bytes = 0;
     int mfma_min_M = 0;
     // the in-launch split-K combine's tile words (tcsc::kCombineBytes, zeroed
@@ -273,9 +274,9 @@ void free_mfma(tcsc_gpu_plan* p) {
 }
 
 void free_csc(tcsc_gpu_plan* p) {
-    for (void* q : {(void*)p->ccp, (void*)p->ccn, (void*)p->crm})
+    for (void* q : {(void*)p->ccq, (void*)p->crq})
         if (q) (void)hipFree(q);
-    p->ccp = p->ccn = p->crm = nullptr;
+    p->ccq = p->crq = nullptr;
     p->csc_bytes = 0;
 }
 
@@ -284,34 +285,46 @@ void free_csc(tcsc_gpu_plan* p) {
 // path and the MFMA path are then off for this plan.
 int build_csc(tcsc_gpu_plan* p, const int* csp, const int* csn, const int* rip, const int* rin, int col_begin,
               hipStream_t st) {
-    if (p->cols == 0) return TCSC_OK;
-    DevBuf trp, trn;  // the rebased per-sign lists, merged into crm
-    if (hipMalloc(&p->ccp, (size_t)(p->cols + 1) * sizeof(int)) != hipSuccess ||
-        hipMalloc(&p->ccn, (size_t)(p->cols + 1) * sizeof(int)) != hipSuccess ||
-        hipMalloc(&p->crm, (size_t)(p->n_pos + p->n_neg > 0 ? p->n_pos + p->n_neg : 1) * sizeof(int)) != hipSuccess ||
+    if (p->cols == 0 || p->rows >= (1 << 28)) return TCSC_OK;  // entries are 4*row (< 2^30) with a sign bit
+    const int nc = p->cols, ng = tcsc::csc_groups(nc);
+    size_t tb = 0;
+    DevBuf tcp, tcn, trp, trn, gq, tmp;  // scratch: the rebased per-sign lists, merged into crq
+    if (tcsc::plan_scan_tmp_bytes(ng + 1, &tb) != hipSuccess || hipMalloc(&p->ccq, (size_t)(ng + 1) * sizeof(int)) != hipSuccess ||
+        tcp.alloc((size_t)(nc + 1) * sizeof(int)) != hipSuccess || tcn.alloc((size_t)(nc + 1) * sizeof(int)) != hipSuccess ||
+        gq.alloc((size_t)(ng + 1) * sizeof(int)) != hipSuccess || tmp.alloc(tb) != hipSuccess ||
         trp.alloc((size_t)(p->n_pos > 0 ? p->n_pos : 1) * sizeof(int)) != hipSuccess ||
         trn.alloc((size_t)(p->n_neg > 0 ? p->n_neg : 1) * sizeof(int)) != hipSuccess) {
         (void)hipGetLastError();
         free_csc(p);
         return TCSC_OK;
     }
-    p->csc_bytes = 2 * (size_t)(p->cols + 1) * sizeof(int) + (size_t)(p->n_pos + p->n_neg) * sizeof(int);
-    HIP_TRY(tcsc::csc_copy(csp, csn, rip, rin, col_begin, p->cols, p->n_pos, p->n_neg, p->ccp, p->ccn,
-                           trp.as<int>(), trn.as<int>(), p->crm, st));
-    HIP_TRY(hipStreamSynchronize(st));  // the temporaries are freed on return
+    HIP_TRY(tcsc::csc_prepare(csp, csn, rip, rin, col_begin, nc, p->n_pos, p->n_neg, tcp.as<int>(), tcn.as<int>(),
+                              trp.as<int>(), trn.as<int>(), gq.as<int>(), tmp.p, tb, p->ccq, st));
+    int quads = 0;
+    HIP_TRY(hipMemcpyAsync(&quads, p->ccq + ng, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const size_t ent = tcsc::csc_quad_entries(quads);
+    if (hipMalloc(&p->crq, ent * sizeof(int)) != hipSuccess) {
+        (void)hipGetLastError();
+        free_csc(p);
+        return TCSC_OK;
+    }
+    p->csc_bytes = (size_t)(ng + 1) * sizeof(int) + ent * sizeof(int);
+    HIP_TRY(tcsc::csc_fill(tcp.as<int>(), tcn.as<int>(), trp.as<int>(), trn.as<int>(), p->ccq, nc, p->rows, p->crq,
+                           ent, st));
+    HIP_TRY(hipStreamSynchronize(st));  // the scratch is freed on return
     return TCSC_OK;
 }
 
-// Small-M path (tcsc_small.hip) on fast-order plans.  It costs ~3 ps per
-// (nonzero, row) at cfg 4's shape (X gathers from L2, one wave per column);
-// the gather costs the same ~256-row tile for any M <= 256 (~0.06 ps per
-// (nonzero, row) of the tile, plus ~20 us of staging and launch).  So: every
-// M <= 4, and M <= 16 while M * nnz <= 2^24 (launch overhead dominates).
-// Measured on one box (tools/small_m.sh): 1 x 512 x 2048 6.5 vs 33.8 us,
-// 4 x 16384^2 (98 %) 62 vs 99 us, 16 x 4096^2 (95 %) 25 vs 34 us,
-// 16 x 16384^2 260 vs 100 us (there the gather stays).  $TCSC_SMALL_M caps M
-// (0 = off).
-constexpr int kSmallMaxM = 16;
+// Small-M path (tcsc_small.hip) on fast-order plans: M <= 4 rows whose X
+// (K + 1 floats a row) fits the LDS, one lane per output column.  The gather
+// costs the same ~256-row tile for any M <= 256 plus ~20 us of staging and
+// launch; the small path's cost grows with M * nnz.  Measured on one box
+// (tools/r5_small.sh, prelu_basic, small vs gather): 1 x 512 x 2048 9.1 vs
+// 39.4 us, 1 x 2048 x 8192 23.0 vs 111 us, 1 x 16384^2 24.5 vs 95 us,
+// 4 x 4096^2 26.0 vs 40.2 us.  M = 4 at K = 16384 does not fit the LDS and
+// stays on the gather.  $TCSC_SMALL_M caps M (0 = off).
+constexpr int kSmallMaxM = 4;
 int small_max_m() {
     const char* e = std::getenv("TCSC_SMALL_M");
     if (!e) return kSmallMaxM;
@@ -319,8 +332,8 @@ int small_max_m() {
 }
 
 bool use_small(const tcsc_gpu_plan* p, int M) {
-    if (!p->ccp || p->rows <= 0 || M < 1 || M > small_max_m() || use_mfma(p, M)) return false;
-    return M <= 4 || (double)M * (double)(p->n_pos + p->n_neg) <= 16777216.0;
+    return p->crq && p->rows > 0 && M >= 1 && M <= small_max_m() && !use_mfma(p, M) &&
+           tcsc::small_m_fits(M, p->rows);
 }
 
 // Adds the MFMA image to a fast-order plan when the path mode and the density
@@ -332,7 +345,7 @@ int maybe_build_mfma(tcsc_gpu_plan* p, const int* csp, const int* csn, const int
     const long long nnz = p->n_pos + p->n_neg;
     if (mode == 1 || cells == 0 || 6.0 * cells > kMfmaMaxImageBytes) return TCSC_OK;
     if (mode == 0 && (nnz < kMfmaDensity * cells || p->rows < 64 || p->cols < 64)) return TCSC_OK;
-    if (!p->ccp) return TCSC_OK;  // the fixup needs the CSC copy
+    if (!p->crq) return TCSC_OK;  // the fixup needs the CSC copy
     const size_t n = (size_t)p->rows * p->cols;
     DevBuf wf, bad;
     if (wf.alloc(n * sizeof(float)) != hipSuccess || bad.alloc(sizeof(int)) != hipSuccess) {
@@ -546,7 +559,7 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
     const bool prelu = is_prelu(variant);
     HIP_TRY(tcsc::mfma_gemm3(x3, p->w3, ldk, M, N, dB, dY, ldy, prelu, a, st));
     // fast order: bias after the sum for every variant
-    HIP_TRY(tcsc::mfma_fixup(x3, M, K, ldk, p->ccp, p->ccn, p->crm, N, dB, dY, ldy, false, prelu, a, flags, st));
+    HIP_TRY(tcsc::mfma_fixup(x3, M, K, ldk, p->ccq, p->crq, N, dB, dY, ldy, false, prelu, a, flags, st));
     return TCSC_OK;
 }
 
@@ -575,8 +588,8 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
             HIP_TRY(hipMemcpyAsync(ws, dX, xb, hipMemcpyDeviceToDevice, st));
             return TCSC_OK;
         }
-        HIP_TRY(tcsc::launch_small_m(stage == 2 ? ws : dX, M, p->rows, p->ccp, p->ccn, p->crm, p->cols, dB, dY, ldy,
-                                     false, is_prelu(variant), a, st));
+        HIP_TRY(tcsc::launch_small_m(stage == 2 ? ws : dX, M, p->rows, p->ccq, p->crq, p->cols, dB, dY, ldy, false,
+                                     is_prelu(variant), a, st));
         return TCSC_OK;
     }
     // gather-path limits: X^T row tiles of 64 rows on the transpose grid's y

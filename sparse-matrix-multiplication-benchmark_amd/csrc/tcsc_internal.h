@@ -250,13 +250,34 @@ int ldxt_for(int M);
 hipError_t launch_transpose(const float* X, int M, int K, float* XT, int ldxt, hipStream_t st);
 
 // ---- per-column CSC copy of a plan's range (small-M path, MFMA fixup) ------
-// cp/cn (ncols+1) and crp/crn (n_pos/n_neg) <- columns [col_begin,
-// col_begin+ncols) of the absolute-offset arrays, rebased; crm (n_pos+n_neg)
-// <- each column's +1 and -1 rows merged in ascending order (the fast
-// order's), -1 rows tagged with bit 31, column j at cp[j] + cn[j].
-hipError_t csc_copy(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int ncols,
-                    long long n_pos, long long n_neg, int* cp, int* cn, int* crp, int* crn, int* crm,
-                    hipStream_t st);
+// The merged list: each column's +1 and -1 rows in ascending order (the fast
+// order's), one entry per nonzero = the row's byte offset 4*k, -1 rows tagged
+// with bit 31, padded with 4*K entries (K = the plan's rows).  Columns go in
+// groups of kCscGroup (a small-M workgroup's lanes), interleaved by 16-B
+// quads: quad q of column j = g*kCscGroup + l sits at int4 index
+// (cq[g] + q) * kCscGroup + l, so the group's quad q is one contiguous 1 KiB.
+// Group g has cq[g+1] - cq[g] quads (its longest column's, rounded up to a
+// multiple of 16: the small-M kernel's unroll); shorter columns are padded.  The array ends with
+// kCscGuardQuads quads of zeros per lane (the small-M kernel's look-ahead).
+// Built in two calls (the host reads cq[ngroups] in between to size crq)
+// from the rebased per-sign lists in the scratch cp/cn (ncols+1), crp/crn.
+constexpr int kCscGroup = 64;
+constexpr int kCscGuardQuads = 16;
+constexpr int kCscRowMask = 0x7fffffff;
+__host__ __device__ inline int csc_groups(int ncols) { return (ncols + kCscGroup - 1) / kCscGroup; }
+inline size_t csc_quad_entries(long long quads) { return (size_t)(quads + kCscGuardQuads) * kCscGroup * 4; }
+// cp, cn, crp, crn and the group quad offsets cq (groups+1) from the column range
+hipError_t csc_prepare(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int ncols,
+                       long long n_pos, long long n_neg, int* cp, int* cn, int* crp, int* crn, int* gq, void* scan_tmp,
+                       size_t scan_tmp_bytes, int* cq, hipStream_t st);
+// crq (csc_quad_entries(cq[groups]) ints) from them
+hipError_t csc_fill(const int* cp, const int* cn, const int* crp, const int* crn, const int* cq, int ncols, int rows,
+                    int* crq, size_t crq_entries, hipStream_t st);
+// column j's entry list in the quad layout: entry i at crq[csc_entry(cq, j, i)]
+__host__ __device__ inline size_t csc_entry(const int* cq, int j, int i) {
+    const int g = j / kCscGroup, l = j % kCscGroup;
+    return ((size_t)(cq[g] + i / 4) * kCscGroup + l) * 4 + (i & 3);
+}
 
 // ---- MFMA path for near-dense W (tcsc_mfma.hip) ------------
 // X3 / W3T rows are ldk = mfma_ldk(K) bf16 long, in blocks of kMfmaBlk = 32
@@ -280,11 +301,15 @@ hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const i
                          int ncols, float* wf, uint16_t* w3, int ldk, long long n_pos, long long n_neg, int* bad,
                          hipStream_t st);
 // ---- small-M path (tcsc_small.hip) ----------------------------
+// X is staged in LDS as M rows of K+1 floats: the path applies only where
+// that fits (at most 160 KiB; 40,959 columns of X at M = 1).
+constexpr size_t small_m_lds_bytes_max() { return 160 * 1024; }
+inline bool small_m_fits(int M, int K) { return M >= 1 && M <= 4 && (size_t)M * (K + 1) * 4 <= small_m_lds_bytes_max(); }
 // Y[m, j] = act(sum over column j's merged rows of +-X[m,k], ascending k,
 // then + B[j]) for m < M <= 16: one lane per column over the merged CSC copy,
 // the fast order's exact arithmetic (bit-identical to k_stream unsplit).
-hipError_t launch_small_m(const float* X, int M, int K, const int* cp, const int* cn, const int* crm, int ncols,
-                          const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a, hipStream_t st);
+hipError_t launch_small_m(const float* X, int M, int K, const int* cq, const int* crq, int ncols, const float* B,
+                          float* Y, int ldy, bool bias_first, bool prelu, float a, hipStream_t st);
 // X (M x K) -> x3 (M x ldk bf16, [h | m | l | 0..]); flags[m] = 1 for the
 // rows the fixup recomputes, 0 otherwise (every row, every call).
 hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int* flags, hipStream_t st);
@@ -292,9 +317,9 @@ hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int
 hipError_t mfma_gemm3(const uint16_t* x3, const uint16_t* w3, int ldk, int M, int N, const float* B, float* Y,
                       int ldy, bool prelu, float a, hipStream_t st);
 // Rewrites the flagged rows in k_stream's fast order (no-op when none is).
-hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cp, const int* cn, const int* crm,
-                      int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
-                      const int* flags, hipStream_t st);
+hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cq, const int* crq, int ncols,
+                      const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a, const int* flags,
+                      hipStream_t st);
 
 // Error channel shared by every entry point of the library (tcsc_api.cpp):
 // the message behind tcsc_gpu_last_error(), and the host API's policy

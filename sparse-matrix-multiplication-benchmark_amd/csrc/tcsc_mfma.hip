@@ -151,21 +151,42 @@ __global__ void k_copy_from(const int* __restrict__ src, const int* __restrict__
         dst[i] = src[base + i];
 }
 
+// gq[g] = quads of group g: its longest column's entries over 4, rounded up
+// to a multiple of 16 quads (the small-M kernel's unroll); gq[groups] = 0.
+__global__ void k_group_quads(const int* __restrict__ cp, const int* __restrict__ cn, int ncols,
+                              int* __restrict__ gq) {
+    const int ng = csc_groups(ncols);
+    for (int g = blockIdx.x * blockDim.x + threadIdx.x; g <= ng; g += gridDim.x * blockDim.x) {
+        int mx = 0;
+        if (g < ng)
+            for (int j = g * kCscGroup; j < min(ncols, (g + 1) * kCscGroup); ++j)
+                mx = max(mx, cp[j + 1] - cp[j] + cn[j + 1] - cn[j]);
+        gq[g] = g < ng ? ((mx + 3) / 4 + 15) & ~15 : 0;
+    }
+}
+
 // Merge each column's +1 and -1 rows (rebased lists rp / rn, offsets cp /
-// cn) into one list in ascending row order, the -1 entries tagged with bit
-// 31, a +1 entry first on a tie (k_scatter's rule), at offset cp[j] + cn[j]:
-// the order in which k_stream's fast order adds a column's nonzeros.
+// cn) into one list in ascending row order -- entries 4*row, the -1 entries
+// tagged with bit 31, a +1 entry first on a tie (k_scatter's rule) -- in the
+// quad layout, padded to its group's length with 4*rows entries: the order in
+// which k_stream's fast order adds a column's nonzeros.
 __global__ void k_merge_csc(const int* __restrict__ cp, const int* __restrict__ cn, const int* __restrict__ rp,
-                            const int* __restrict__ rn, int ncols, int* __restrict__ rm) {
+                            const int* __restrict__ rn, const int* __restrict__ cq, int ncols, int rows,
+                            int* __restrict__ rm) {
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < ncols; j += gridDim.x * blockDim.x) {
-        int p = cp[j], q = cn[j], o = cp[j] + cn[j];
+        const int g = j / kCscGroup;
+        const int n = 4 * (cq[g + 1] - cq[g]);
+        int p = cp[j], q = cn[j], i = 0;
         const int p1 = cp[j + 1], q1 = cn[j + 1];
         while (p < p1 || q < q1) {
+            int e;
             if (q >= q1 || (p < p1 && rp[p] <= rn[q]))
-                rm[o++] = rp[p++];
+                e = 4 * rp[p++];
             else
-                rm[o++] = (int)((unsigned)rn[q++] | 0x80000000u);
+                e = (int)((unsigned)(4 * rn[q++]) | 0x80000000u);
+            rm[csc_entry(cq, j, i++)] = e;
         }
+        for (; i < n; ++i) rm[csc_entry(cq, j, i)] = 4 * rows;
     }
 }
 
@@ -173,19 +194,21 @@ __global__ void k_merge_csc(const int* __restrict__ cp, const int* __restrict__ 
 // comment): x rebuilt from its three parts, the column's merged rows in
 // ascending k, the bias first or last, then the PReLU.
 template <bool BIAS_FIRST, bool PRELU>
-__device__ inline float exact_out(const uint16_t* __restrict__ X3, int K, int ldk, const int* __restrict__ cp,
-                                  const int* __restrict__ cn, const int* __restrict__ rm,
-                                  const float* __restrict__ Bias, int row, int j, float a) {
+__device__ inline float exact_out(const uint16_t* __restrict__ X3, int K, int ldk, const int* __restrict__ cq,
+                                  const int* __restrict__ rm, const float* __restrict__ Bias, int row, int j,
+                                  float a) {
     const uint16_t* x3 = X3 + (size_t)row * ldk;
     auto xk = [&](int k) {
         return (u2f((uint32_t)x3[x3_index(k, 0)] << 16) + u2f((uint32_t)x3[x3_index(k, 1)] << 16)) +
                u2f((uint32_t)x3[x3_index(k, 2)] << 16);
     };
     float acc = BIAS_FIRST ? Bias[j] : 0.0f;
-    const int e1 = cp[j + 1] + cn[j + 1];
-    for (int e = cp[j] + cn[j]; e < e1; ++e) {
-        const int r = rm[e];
-        acc = fmaf(xk(r & 0x7fffffff), r < 0 ? -1.0f : 1.0f, acc);
+    const int g = j / kCscGroup, n = 4 * (cq[g + 1] - cq[g]);
+    for (int i = 0; i < n; ++i) {
+        const int r = rm[csc_entry(cq, j, i)];
+        const int k = (r & kCscRowMask) >> 2;
+        if (k >= K) break;  // the column's padding
+        acc = fmaf(xk(k), r < 0 ? -1.0f : 1.0f, acc);
     }
     if (!BIAS_FIRST) acc += Bias[j];
     if (PRELU) acc = (acc < 0.0f) ? a * acc : acc;
@@ -197,8 +220,8 @@ __device__ inline float exact_out(const uint16_t* __restrict__ X3, int K, int ld
 // none and the kernel ends there.
 template <bool BIAS_FIRST, bool PRELU>
 __global__ void __launch_bounds__(256) k_fixup(const uint16_t* __restrict__ X3, int M, int K, int ldk,
-                                               const int* __restrict__ cp, const int* __restrict__ cn,
-                                               const int* __restrict__ rm, int ncols,
+                                               const int* __restrict__ cq, const int* __restrict__ rm,
+                                               int ncols,
                                                const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a,
                                                const int* __restrict__ flags) {
     int any = 0;
@@ -208,7 +231,7 @@ __global__ void __launch_bounds__(256) k_fixup(const uint16_t* __restrict__ X3, 
     if (j >= ncols) return;
     for (int row = 0; row < M; ++row)
         if (flags[row])
-            Y[(size_t)row * ldy + j] = exact_out<BIAS_FIRST, PRELU>(X3, K, ldk, cp, cn, rm, Bias, row, j, a);
+            Y[(size_t)row * ldy + j] = exact_out<BIAS_FIRST, PRELU>(X3, K, ldk, cq, rm, Bias, row, j, a);
 }
 
 // ---------------------------------------------------------------------------
@@ -346,9 +369,9 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
 
 }  // namespace
 
-hipError_t csc_copy(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int ncols,
-                    long long n_pos, long long n_neg, int* cp, int* cn, int* crp, int* crn, int* crm,
-                    hipStream_t st) {
+hipError_t csc_prepare(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int ncols,
+                       long long n_pos, long long n_neg, int* cp, int* cn, int* crp, int* crn, int* gq, void* scan_tmp,
+                       size_t scan_tmp_bytes, int* cq, hipStream_t st) {
     hipError_t e;
     if ((e = rebase_offsets(csp, col_begin, ncols, cp, st)) != hipSuccess) return e;
     if ((e = rebase_offsets(csn, col_begin, ncols, cn, st)) != hipSuccess) return e;
@@ -356,9 +379,20 @@ hipError_t csc_copy(const int* csp, const int* csn, const int* rip, const int* r
         hipLaunchKernelGGL(k_copy_from, dim3(grid_of(n_pos, 256)), dim3(256), 0, st, rip, csp, col_begin, n_pos, crp);
     if (n_neg > 0)
         hipLaunchKernelGGL(k_copy_from, dim3(grid_of(n_neg, 256)), dim3(256), 0, st, rin, csn, col_begin, n_neg, crn);
+    const int ng = csc_groups(ncols);
+    hipLaunchKernelGGL(k_group_quads, dim3(grid_of((long long)ng + 1, 256)), dim3(256), 0, st, cp, cn, ncols, gq);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (ncols > 0 && n_pos + n_neg > 0)
-        hipLaunchKernelGGL(k_merge_csc, dim3(grid_of(ncols, 256)), dim3(256), 0, st, cp, cn, crp, crn, ncols, crm);
+    return exclusive_scan_i32(gq, cq, ng + 1, scan_tmp, scan_tmp_bytes, st);
+}
+
+hipError_t csc_fill(const int* cp, const int* cn, const int* crp, const int* crn, const int* cq, int ncols, int rows,
+                    int* crq, size_t crq_entries, hipStream_t st) {
+    hipError_t e;
+    // the guard quads (and nothing else) stay 0: row 0, read only by the look-ahead
+    if ((e = hipMemsetAsync(crq, 0, crq_entries * sizeof(int), st)) != hipSuccess) return e;
+    if (ncols > 0)
+        hipLaunchKernelGGL(k_merge_csc, dim3(grid_of(ncols, 256)), dim3(256), 0, st, cp, cn, crp, crn, cq, ncols, rows,
+                           crq);
     return hipGetLastError();
 }
 
@@ -413,11 +447,11 @@ hipError_t mfma_gemm3(const uint16_t* x3, const uint16_t* w3, int ldk, int M, in
                  : launch_gemm3_t<false>(x3, w3, ldk, M, N, B, Y, ldy, a, st);
 }
 
-hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cp, const int* cn, const int* crm,
-                      int ncols, const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a,
-                      const int* flags, hipStream_t st) {
+hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cq, const int* crq, int ncols,
+                      const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a, const int* flags,
+                      hipStream_t st) {
     const dim3 grid((ncols + 255) / 256), block(256);
-#define TCSC_FIX_ARGS x3, M, K, ldk, cp, cn, crm, ncols, B, Y, ldy, a, flags
+#define TCSC_FIX_ARGS x3, M, K, ldk, cq, crq, ncols, B, Y, ldy, a, flags
     if (bias_first) {
         if (prelu)
             hipLaunchKernelGGL((k_fixup<true, true>), grid, block, 0, st, TCSC_FIX_ARGS);

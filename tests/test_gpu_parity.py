@@ -164,8 +164,14 @@ def test_prepare_then_gather_equals_sgemm(gpu, torch_cuda, name):
 def test_multi_shard_host_path_equals_single(gpu, shards, axis, monkeypatch):
     """The host API's blocks (one per GPU on a node; several per device here)
     concatenate to the single-block result bit for bit: column blocks
-    (TCSC_SHARD_AXIS=cols, the default) and row blocks."""
+    (TCSC_SHARD_AXIS=cols, the default) and row blocks.  Row blocks of a few
+    rows take the small-M path, whose sums are in the fast order; the whole
+    launch is held to the same order (the gather, K unsplit) so that the
+    comparison is bit for bit whatever path a block's M selects."""
     monkeypatch.setenv("TCSC_SHARD_AXIS", axis)
+    if axis == "rows":
+        monkeypatch.setenv("TCSC_PATH", "gather")
+        monkeypatch.setenv("TCSC_SLICES", "1")
     g = load_golden("grid_m16_k512_n1024_nz8")
     W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
     tcsc_amd.set_num_shards(1)

@@ -1,6 +1,7 @@
-"""The small-M path (csrc/tcsc_small.hip): M <= 4 (and M <= 16
-while M * nnz <= 2^24) runs one wave per output column over the plan's CSC
-copy instead of the 256-row gather.  Same bars as the gather: float outputs
+"""The small-M path (csrc/tcsc_small.hip): M <= 4 rows whose
+X fits the LDS run one lane per output column over the plan's merged CSC
+copy instead of the 256-row gather (M = 7 and 16 below check the hand-over
+to the gather).  Same bars as the gather: float outputs
 within 2^-20 * (|b| + sum|x|) of the exact sums, integer inputs bit-exact
 with the reference's outputs for all five variants, NaN/inf classified as
 the reference does; the prepared (prepare_x + sgemm_prepared) form and
