@@ -487,23 +487,28 @@ __device__ __forceinline__ unsigned long long rtstamp() {
 #endif
 
 // In-launch split-K combine (k_stream OUT 2; DESIGN.md §4 k_reduce).  The
-// Z workgroups of a tile (its K slices) each write their slab with sc1
-// (write-through) stores, drain them (vmcnt(0) in every wave, barrier) and
-// add 1 to the tile's arrival word (lane 0, agent scope).  Each then owns
-// row band z of the tile: it polls the arrival word (sc1 loads, s_sleep)
-// until all Z have arrived, claims its band (compare-and-swap 0 -> 1) and
-// reduces it from all Z slabs with sc1 loads -- the same adds in the same
-// order as k_reduce4, so the same bits.  The workgroup whose add came last
-// knows the slabs are complete without polling; after its own band it
-// claims and reduces any band still unclaimed, so a workgroup whose poll
-// gives up (after kCombineWaitTicks of wall time, ~50 us: a slice that is not
-// resident, or TCSC_COMBINE_GIVEUP) leaves no band undone, and no band is
-// reduced twice.  The last workgroup to finish
-// (the done word) zeroes the tile's words for the next launch.  The host
-// takes this path only when the grid fits the chip at one workgroup per CU
+// Z workgroups of a tile (its K slices) each own row band z of the tile.
+// Each writes the other bands of its slab with sc1 (write-through) stores;
+// at Z = 4 (a band is exactly one 64-row epilogue pass) its own band stays
+// in the LDS, otherwise it is written too.  It drains the stores (vmcnt(0)
+// in every wave, barrier) and adds 1 to the tile's arrival word (lane 0,
+// agent scope), then polls the arrival word (sc1 loads, s_sleep) until all
+// Z have arrived, marks its band taken (state word 1) and reduces it: its
+// own partial from the LDS, the others' from their slabs with sc1 loads --
+// the same adds in the same order as k_reduce4, so the same bits.  A
+// workgroup whose poll gives up (after kCombineWaitTicks of wall time, ~50
+// us: a slice that is not resident, or TCSC_COMBINE_GIVEUP) first writes its
+// own band to its slab (sc1, drained, barrier) and then marks it abandoned
+// (state 2).  The workgroup whose add came last knows the slabs are
+// complete without polling; after its own band it waits for every other
+// band's state word to leave 0 (each owner is running: it has arrived) and
+// reduces the abandoned ones from the slabs, so no band is left undone and
+// none is reduced twice.  The last workgroup to finish (the done word)
+// zeroes the tile's words for the next launch.  The host takes this path
+// only when the grid fits the chip at one workgroup per CU
 // (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility",
-// the counter hand-off row: sc1 stores, vmcnt(0), barrier, one agent add,
-// sc1 poll or the add's return value, barrier, sc1 loads).
+// the counter hand-off row: sc1 stores, vmcnt(0), barrier, one agent add or
+// store, sc1 poll or the add's return value, barrier, sc1 loads).
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4c_t __attribute__((ext_vector_type(4)));
 constexpr int kSc1 = 16;  // buffer cache-policy bits: sc1
@@ -523,12 +528,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t slabs_rsrc(float* ws, int Z, i
     return __builtin_amdgcn_make_buffer_rsrc(ws, 0, (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL), 0x00020000);
 }
 
+// The tile's own band at Z = 4 (k_stream's epilogue keeps it there): row R
+// of the band at byte kOwnBandOff + R * 1 KiB, column j at + 4 j.
+constexpr int kOwnBandOff = kWaves * 64 * (kCW * 4 + 16);  // past the epilogue's 64-row staging
+static_assert(kOwnBandOff + 64 * kRowBytes <= kLdsBytes - 16, "the own band fits beside the epilogue staging");
+
 template <bool BIAS_FIRST, bool PRELU>
 __device__ __forceinline__ void combine_tile(float* ws, int M, int ncols, const float* __restrict__ Bias,
                                              float* __restrict__ Y, int ldy, float a, unsigned* ccnt, const Tile t,
-                                             char* lds, int giveup) {
+                                             char* lds, int giveup, bool own_lds) {
     const int Z = (int)gridDim.z;
-    unsigned* w = ccnt + (size_t)(t.rt * (int)gridDim.x + t.cb) * kCombineWords;  // {arrivals, done, claims[Z]}
+    unsigned* w = ccnt + (size_t)(t.rt * (int)gridDim.x + t.cb) * kCombineWords;  // {arrivals, done, state[Z]}
     int* flag = reinterpret_cast<int*>(lds);  // the epilogue's staging is done (barrier below)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores have left
     __syncthreads();
@@ -546,6 +556,7 @@ __device__ __forceinline__ void combine_tile(float* ws, int M, int ncols, const 
                 __builtin_amdgcn_s_sleep(4);
             }
         }
+        if (st != 0) __hip_atomic_store(w + 2 + t.z, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         flag[0] = st;
     }
     __syncthreads();
@@ -553,20 +564,8 @@ __device__ __forceinline__ void combine_tile(float* ws, int M, int ncols, const 
     const __amdgpu_buffer_rsrc_t rs = slabs_rsrc(ws, Z, M, ncols);
     const int m0 = t.rt * kTM, c0 = t.cb * kWgCols;
     const size_t slab = (size_t)M * ncols;
-    auto claim = [&](int q) {
-        __syncthreads();  // everyone has read the previous flag
-        if (threadIdx.x == 0) {
-            unsigned expect = 0u;
-            flag[1] = __hip_atomic_compare_exchange_strong(w + 2 + q, &expect, 1u, __ATOMIC_RELAXED,
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                          ? 1
-                          : 0;
-        }
-        __syncthreads();
-        return __builtin_amdgcn_readfirstlane(flag[1]) != 0;
-    };
-    auto reduce_band = [&](int q) {
-        constexpr int nq = kWgCols / 4;
+    constexpr int nq = kWgCols / 4;
+    auto reduce_band = [&](int q, bool own) {  // own: slab q's band q is in this workgroup's LDS
         const int r0 = kTM * q / Z, r1 = kTM * (q + 1) / Z;
         for (int i = threadIdx.x; i < (r1 - r0) * nq; i += kWaves * 64) {
             const int row = m0 + r0 + i / nq, col = c0 + 4 * (i % nq);
@@ -575,9 +574,14 @@ __device__ __forceinline__ void combine_tile(float* ws, int M, int ncols, const 
             f32x4c_t p[16];
 #pragma unroll
             for (int s = 0; s < 16; ++s)
-                if (s < Z)
-                    p[s] = __builtin_bit_cast(
-                        f32x4c_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off, (int)(s * slab * 4), kSc1));
+                if (s < Z) {
+                    if (own && s == q)
+                        p[s] = *reinterpret_cast<const f32x4c_t*>(lds + kOwnBandOff + (i / nq) * kRowBytes +
+                                                                  16 * (i % nq));
+                    else
+                        p[s] = __builtin_bit_cast(
+                            f32x4c_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off, (int)(s * slab * 4), kSc1));
+                }
             const float4 b = *reinterpret_cast<const float4*>(Bias + col);
             float4 v = BIAS_FIRST ? b : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -605,10 +609,45 @@ __device__ __forceinline__ void combine_tile(float* ws, int M, int ncols, const 
             __builtin_nontemporal_store(o, reinterpret_cast<nt4*>(Y + (size_t)row * ldy + col));
         }
     };
-    if (st != 0 && claim(t.z)) reduce_band(t.z);
-    if (st == 2)
-        for (int q = 0; q < Z; ++q)
-            if (q != t.z && claim(q)) reduce_band(q);
+    if (st != 0) {
+        reduce_band(t.z, own_lds);
+    } else {
+        if (own_lds) {
+            // give the band up: its LDS partial into slab t.z (sc1), drained by every wave
+            const int r0 = kTM * t.z / Z, r1 = kTM * (t.z + 1) / Z;
+            for (int i = threadIdx.x; i < (r1 - r0) * nq; i += kWaves * 64) {
+                const int row = m0 + r0 + i / nq, col = c0 + 4 * (i % nq);
+                if (row >= M || col >= ncols) continue;
+                const int off = (int)(((size_t)t.z * M + row) * ncols + col) * 4;
+                const f32x4c_t v =
+                    *reinterpret_cast<const f32x4c_t*>(lds + kOwnBandOff + (i / nq) * kRowBytes + 16 * (i % nq));
+                // whole quads: the host combines in launch only when ncols % 4 == 0
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rs, off, 0, kSc1);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) __hip_atomic_store(w + 2 + t.z, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (st == 2) {
+        // every other owner has arrived, so it is running and will mark its band
+        // taken or abandoned; the bound (100 ms) only keeps a broken launch from
+        // hanging the device
+        for (int q = 0; q < Z; ++q) {
+            if (q == t.z) continue;
+            __syncthreads();  // everyone has read the previous flag
+            if (threadIdx.x == 0) {
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                unsigned v;
+                while ((v = __hip_atomic_load(w + 2 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u &&
+                       __builtin_amdgcn_s_memrealtime() - t0 < 10000000ull)
+                    __builtin_amdgcn_s_sleep(2);
+                flag[1] = (int)v;
+            }
+            __syncthreads();
+            if (__builtin_amdgcn_readfirstlane(flag[1]) == 2) reduce_band(q, false);
+        }
+    }
     __syncthreads();
     if (threadIdx.x == 0 && __hip_atomic_fetch_add(w + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 ==
                                 (unsigned)Z) {
@@ -805,6 +844,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     // both words, and writes Y = act((0 + s0) + s1 + b) from its registers
     // and the partner's slab, in slice order -- k_reduce4's adds, the same
     // bits.  The first finisher never waits, so no residency is assumed.
+    const bool own_lds = OUT == 2 && gridDim.z == 4;  // combine_tile: the own band stays in the LDS
     int pair_role = 0;  // OUT 3: 0 = store the slab, 1 = combine
     unsigned* const pw = OUT == 3 ? ccnt + (size_t)(t.rt * (int)gridDim.x + t.cb) * kCombineWords : nullptr;
     auto epilogue = [&](auto how_) {
@@ -941,9 +981,14 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                             }
                         } else if constexpr (OUT == 2) {
                             // write-through (sc1) slab stores: the tile's other
-                            // workgroups read them with sc1 loads (combine_tile)
+                            // workgroups read them with sc1 loads (combine_tile);
+                            // at Z = 4 the own band (pass h == z) stays in the LDS
                             const int off = (int)(((size_t)t.z * M + row) * ncols + col) * 4;
-                            if (vec_ok && col + 3 < col_end) {
+                            if (own_lds && h == t.z) {
+                                static_assert(kEpiRows == 64, "a pass is one band at Z = 4");
+                                *reinterpret_cast<float4*>(lds + kOwnBandOff + R * kRowBytes +
+                                                           (col - t.cb * kWgCols) * 4) = v;
+                            } else if (vec_ok && col + 3 < col_end) {
                                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), slab_rs, off, 0,
                                                                        kSc1);
                             } else {
@@ -986,7 +1031,8 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
 #ifdef TCSC_STAMPS
         rt_[3] = rtstamp();
 #endif
-        if constexpr (OUT == 2) combine_tile<BIAS_FIRST, PRELU>(ws, M, ncols, Bias, Y, ldy, a, ccnt, t, lds, combine_giveup);
+        if constexpr (OUT == 2) combine_tile<BIAS_FIRST, PRELU>(ws, M, ncols, Bias, Y, ldy, a, ccnt, t, lds, combine_giveup,
+                                                         own_lds);
         if constexpr (OUT == 3) {
             if (pair_role == 0) {  // publish the slab: every wave's sc1 stores drained, then one agent add
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -57,6 +57,7 @@ SHAPES = [  # M, K, N, density, variant, forced slices
     (1024, 4096, 4096, 0.05, "prelu_separate", "2"),    # bias last, two row bands
     (300, 1000, 200, 0.05, "prelu_onthego", None),      # ragged M, one partial column block
     (513, 2400, 700, 0.1, "basic", "3"),                # forced 3 slices: bands of 85/85/86 rows
+    (517, 2400, 700, 0.1, "prelu_basic", "4"),          # 4 slices (own band kept in the LDS), ragged M and N
     (1024, 16384, 1024, 0.02, "prelu_basic", "16"),     # 16 slices x 16 tiles = 256 workgroups
     (4096, 16384, 2048, 0.02, "prelu_basic", None),     # the 8-way column block of cfg 4
     (2048, 4096, 8192, 0.05, "basic", "2"),             # 1024 workgroups: no combine, same bits
@@ -173,6 +174,7 @@ def test_launch_combine_reports_the_path(gpu, monkeypatch, M, K, N, density, env
 @pytest.mark.parametrize("M,K,N,density,variant,slices", [
     (1024, 4096, 4096, 0.05, "prelu_basic", None),      # cfg 3: 4 slices
     (513, 2400, 700, 0.1, "basic", "3"),                # uneven bands
+    (517, 2400, 700, 0.1, "prelu_basic", "4"),          # own bands written out on giving up, ragged M
     (1024, 16384, 1024, 0.02, "prelu_separate", "16"),  # 16 slices: one workgroup reduces all 16 bands
     (4096, 16384, 2048, 0.02, "prelu_basic", "2"),      # the 8-way column block
 ])
