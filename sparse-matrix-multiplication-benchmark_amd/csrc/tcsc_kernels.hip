@@ -829,10 +829,10 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     // Epilogue: lanes hold rows (4 per lane), so a direct store would put
     // 64 rows' 4-byte pieces in one instruction (partial-line writes that
     // cost ~16x the bytes in HBM writes).  Transpose through LDS instead:
-    // per pass of kEpiRows rows every wave parks its kEpiRows x kCW block
-    // (row stride kCW*4 + 16 B, so the b128 writes of consecutive lanes,
-    // 4 rows apart, spread over the banks), then reads it back as rows:
-    // kCW/4 lanes per row, 16-B stores.
+    // per pass of 64 rows every wave parks its 64 x kCW block into the
+    // pass's tile rows (1 KiB + 16 B apart), then each wave reads back whole
+    // tile rows (wave, wave + 16, ...): lane l stores columns 4l..4l+3, so
+    // one store instruction writes one full 1-KiB row.
     // HOW: 0 the final values (bias last unless BIAS_FIRST, PReLU); 1 (order 2,
     // after the +1 chain) acc + bias parked in Y as is; 2 (order 2, after the
     // -1 chain) the parked value + acc, then PReLU.  A thread re-reads in
@@ -869,21 +869,28 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
             __syncthreads();
             pair_role = __builtin_amdgcn_readfirstlane(role[0]);
         }
-        constexpr int kQ = kCW / 4;                 // 16-B quads per row
-        constexpr int kStride = kCW * 4 + 16;       // bytes per parked row
-        constexpr int kEpiRows = (kWaves * 128 * kStride <= kLdsBytes) ? 128 : 64;
-        static_assert(kWaves * kEpiRows * kStride <= kLdsBytes, "epilogue staging fits the LDS");
+        constexpr int kQ = kCW / 4;                 // 16-B quads of a wave's row
+        constexpr int kEpiRows = 64;                // tile rows per pass
+        constexpr int kStride = kRowBytes + 16;     // bytes per parked tile row
+        static_assert(kEpiRows * kStride <= kOwnBandOff, "the epilogue staging stays below the own band");
+        static_assert(kEpiRows % kWaves == 0 && kWgCols == 64 * 4, "each wave stores whole tile rows");
         constexpr int kLanesPerPass = kEpiRows / 4;
-        constexpr int kRowsPerRead = 64 / kQ;       // rows one read instruction covers
-        char* region = lds + wave * (kEpiRows * kStride);
-        const int col0 = group_col0(g);
-        const int col_end = min(col0 + wave_cols(wave), ncols);  // this wave's columns: [col0, col_end)
+        const int pcol = group_col0(g) - t.cb * kWgCols;  // this wave's first column in a parked row
+        const int col = t.cb * kWgCols + 4 * lane;        // the lane's 4 columns of a stored tile row
+        const int col_end = ncols;
         const bool vec_ok = OUT == 0 ? ((ldy & 3) == 0 && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0))
                                      : ((ncols & 3) == 0 && ((reinterpret_cast<uintptr_t>(ws) & 15) == 0));
         const __amdgpu_buffer_rsrc_t slab_rs = slabs_rsrc(ws, (int)gridDim.z, M, ncols);
         constexpr bool kAddBias = OUT == 0 && (HOW == 1 || (HOW == 0 && !BIAS_FIRST));
         constexpr bool kPrelu = PRELU && HOW != 1;
         constexpr bool kLoadBias = kAddBias || OUT == 3;
+        float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (kLoadBias) {
+            bq.x = col + 0 < col_end ? Bias[col + 0] : 0.f;
+            bq.y = col + 1 < col_end ? Bias[col + 1] : 0.f;
+            bq.z = col + 2 < col_end ? Bias[col + 2] : 0.f;
+            bq.w = col + 3 < col_end ? Bias[col + 3] : 0.f;
+        }
 #pragma unroll
         for (int h = 0; h < 256 / kEpiRows; ++h) {
             if (active && lane / kLanesPerPass == h) {
@@ -896,27 +903,17 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                         const float4 v =
                             make_float4(acc_get(acc, 4 * (4 * q + 0) + r), acc_get(acc, 4 * (4 * q + 1) + r),
                                         acc_get(acc, 4 * (4 * q + 2) + r), acc_get(acc, 4 * (4 * q + 3) + r));
-                        *reinterpret_cast<float4*>(region + R * kStride + q * 16) = v;
+                        *reinterpret_cast<float4*>(lds + R * kStride + pcol * 4 + q * 16) = v;
                     }
                 }
             }
             __syncthreads();
-            if (active && lane < kRowsPerRead * kQ) {
-                const int q = lane % kQ;
-                const int col = col0 + 4 * q;
-                float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (kLoadBias) {
-                    bq.x = col + 0 < col_end ? Bias[col + 0] : 0.f;
-                    bq.y = col + 1 < col_end ? Bias[col + 1] : 0.f;
-                    bq.z = col + 2 < col_end ? Bias[col + 2] : 0.f;
-                    bq.w = col + 3 < col_end ? Bias[col + 3] : 0.f;
-                }
-#pragma unroll 4
-                for (int i = 0; i < (kEpiRows + kRowsPerRead - 1) / kRowsPerRead; ++i) {
-                    const int R = lane / kQ + kRowsPerRead * i;
+            {
+#pragma unroll
+                for (int i = 0; i < kEpiRows / kWaves; ++i) {
+                    const int R = wave + kWaves * i;  // whole 1-KiB tile rows: one full-line store per wave
                     const int row = m0 + kEpiRows * h + R;
-                    if (R >= kEpiRows) break;
-                    float4 v = *reinterpret_cast<const float4*>(region + R * kStride + q * 16);
+                    float4 v = *reinterpret_cast<const float4*>(lds + R * kStride + lane * 16);
                     if (row < M && col < col_end) {
                         float* dst;
                         if (OUT == 0) {
