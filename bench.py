@@ -249,7 +249,10 @@ def main():
         try:
             with open(args.traffic) as f:
                 t = json.load(f)
+            # a row block (--shard rows) is its own launch shape: keyed by its rows too
             key = f"cfg{cfg.idx}:{variant}:{ncols}"
+            if cfg.M != workloads.CONFIGS[cfg.idx].M:
+                key += f":M{cfg.M}"
             if key in t:
                 traffic = t[key]["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
