@@ -61,6 +61,11 @@ def test_reference_main_cpp_validates_every_case():
     live = None
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
         live = open(os.path.join(ROOT, "gpurun_out", "main_amd_out.txt"), "w", buffering=1)
+        # the "GEMM" timing lines below are not the reference's protocol
+        live.write("# main_amd_rv: validation by the reference's dense.c; the GEMM timing lines time the "
+                   "library's bit-identical gemm_basic restatement on all usable cores "
+                   "(TCSC_DENSE_THREADS=0), not dense.c single-threaded: its GEMM times and the "
+                   "speedups against them are not comparable with an upstream run\n")
     # a pseudo-terminal would make the harness's stdout line-buffered, but a
     # GPU box may have none: a pipe (its output arrives in 4-KiB blocks) plus
     # a heartbeat line in the live log every 20 s
