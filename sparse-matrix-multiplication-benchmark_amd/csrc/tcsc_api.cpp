@@ -316,14 +316,14 @@ int build_csc(tcsc_gpu_plan* p, const int* csp, const int* csn, const int* rip, 
     return TCSC_OK;
 }
 
-// Small-M path (tcsc_small.hip) on fast-order plans: M <= 4 rows whose X
-// (K + 1 floats a row) fits the LDS, one lane per output column.  The gather
-// costs the same ~256-row tile for any M <= 256 plus ~20 us of staging and
-// launch; the small path's cost grows with M * nnz.  Measured on one box
-// (tools/r5_small.sh, prelu_basic, small vs gather): 1 x 512 x 2048 9.1 vs
-// 39.4 us, 1 x 2048 x 8192 23.0 vs 111 us, 1 x 16384^2 24.5 vs 95 us,
-// 4 x 4096^2 26.0 vs 40.2 us.  M = 4 at K = 16384 does not fit the LDS and
-// stays on the gather.  $TCSC_SMALL_M caps M (0 = off).
+// Small-M path (tcsc_small.hip) on fast-order plans: M <= 4 rows whose X and
+// -X fit the LDS, one lane per output column.  The gather costs the same
+// ~256-row tile for any M <= 256 plus ~20 us of staging and launch; the small
+// path's cost grows with M * nnz.  Measured on one box (tools/r5_small.sh,
+// prelu_basic, small vs gather): 1 x 512 x 2048 7.9 vs 36.8 us, 1 x 2048 x
+// 8192 16.1 vs 111 us, 1 x 16384^2 15.0 vs 93 us, 4 x 4096^2 15.1 vs 36.4 us.
+// M = 4 at K = 16384 does not fit the LDS and stays on the gather.
+// $TCSC_SMALL_M caps M (0 = off).
 constexpr int kSmallMaxM = 4;
 int small_max_m() {
     const char* e = std::getenv("TCSC_SMALL_M");

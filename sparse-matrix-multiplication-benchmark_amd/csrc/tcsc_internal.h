@@ -251,19 +251,24 @@ hipError_t launch_transpose(const float* X, int M, int K, float* XT, int ldxt, h
 
 // ---- per-column CSC copy of a plan's range (small-M path, MFMA fixup) ------
 // The merged list: each column's +1 and -1 rows in ascending order (the fast
-// order's), one entry per nonzero = the row's byte offset 4*k, -1 rows tagged
-// with bit 31, padded with 4*K entries (K = the plan's rows).  Columns go in
+// order's), one entry per nonzero: 4*k for a +1 row, 4*Kp + 4*k for a -1 row
+// (Kp = K + 1 rounded up to a multiple of 4), padded with 4*K entries (K = the
+// plan's rows, < 2^28).  An entry is the byte offset of +X[k] or -X[k] in a
+// staged row pair [X | -0.0 | 0.. | -X | 0..] of 2*Kp floats (the small-M
+// kernel's LDS rows, both halves 16-B aligned; padding reads the -0.0).  Columns go in
 // groups of kCscGroup (a small-M workgroup's lanes), interleaved by 16-B
 // quads: quad q of column j = g*kCscGroup + l sits at int4 index
 // (cq[g] + q) * kCscGroup + l, so the group's quad q is one contiguous 1 KiB.
 // Group g has cq[g+1] - cq[g] quads (its longest column's, rounded up to a
-// multiple of 16: the small-M kernel's unroll); shorter columns are padded.  The array ends with
-// kCscGuardQuads quads of zeros per lane (the small-M kernel's look-ahead).
+// multiple of 16: the small-M kernel's unroll); shorter columns are padded.
+// The array ends with kCscGuardQuads quads of zeros per lane (the small-M
+// kernel's look-ahead reads that far past a group).
 // Built in two calls (the host reads cq[ngroups] in between to size crq)
 // from the rebased per-sign lists in the scratch cp/cn (ncols+1), crp/crn.
 constexpr int kCscGroup = 64;
-constexpr int kCscGuardQuads = 16;
-constexpr int kCscRowMask = 0x7fffffff;
+constexpr int kCscGuardQuads = 48;
+__host__ __device__ inline int csc_half(int K) { return (K + 4) & ~3; }     // Kp: floats per half of a row pair
+__host__ __device__ inline int csc_neg_base(int K) { return 4 * csc_half(K); }  // a -1 row's offset: -X[k] at 4Kp + 4k
 __host__ __device__ inline int csc_groups(int ncols) { return (ncols + kCscGroup - 1) / kCscGroup; }
 inline size_t csc_quad_entries(long long quads) { return (size_t)(quads + kCscGuardQuads) * kCscGroup * 4; }
 // cp, cn, crp, crn and the group quad offsets cq (groups+1) from the column range
@@ -301,12 +306,14 @@ hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const i
                          int ncols, float* wf, uint16_t* w3, int ldk, long long n_pos, long long n_neg, int* bad,
                          hipStream_t st);
 // ---- small-M path (tcsc_small.hip) ----------------------------
-// X is staged in LDS as M rows of K+1 floats: the path applies only where
-// that fits (at most 160 KiB; 40,959 columns of X at M = 1).
+// X is staged in LDS as M row pairs [X | -0.0 | 0.. | -X | 0..] of 2*Kp
+// floats: the path applies only where that fits (at most 160 KiB; K < 20,477
+// at M = 1).
 constexpr size_t small_m_lds_bytes_max() { return 160 * 1024; }
-inline bool small_m_fits(int M, int K) { return M >= 1 && M <= 4 && (size_t)M * (K + 1) * 4 <= small_m_lds_bytes_max(); }
+inline size_t small_m_lds_bytes(int M, int K) { return (size_t)M * 2 * (size_t)csc_half(K) * 4; }
+inline bool small_m_fits(int M, int K) { return M >= 1 && M <= 4 && small_m_lds_bytes(M, K) <= small_m_lds_bytes_max(); }
 // Y[m, j] = act(sum over column j's merged rows of +-X[m,k], ascending k,
-// then + B[j]) for m < M <= 16: one lane per column over the merged CSC copy,
+// then + B[j]) for m < M <= 4: one lane per column over the merged CSC copy,
 // the fast order's exact arithmetic (bit-identical to k_stream unsplit).
 hipError_t launch_small_m(const float* X, int M, int K, const int* cq, const int* crq, int ncols, const float* B,
                           float* Y, int ldy, bool bias_first, bool prelu, float a, hipStream_t st);

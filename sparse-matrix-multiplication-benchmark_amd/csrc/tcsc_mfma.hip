@@ -166,10 +166,10 @@ __global__ void k_group_quads(const int* __restrict__ cp, const int* __restrict_
 }
 
 // Merge each column's +1 and -1 rows (rebased lists rp / rn, offsets cp /
-// cn) into one list in ascending row order -- entries 4*row, the -1 entries
-// tagged with bit 31, a +1 entry first on a tie (k_scatter's rule) -- in the
-// quad layout, padded to its group's length with 4*rows entries: the order in
-// which k_stream's fast order adds a column's nonzeros.
+// cn) into one list in ascending row order -- entries 4*row for +1 rows and
+// csc_neg_base(rows) + 4*row for -1 rows, a +1 entry first on a tie (k_scatter's
+// rule) -- in the quad layout, padded to its group's length with 4*rows
+// entries: the order in which k_stream's fast order adds a column's nonzeros.
 __global__ void k_merge_csc(const int* __restrict__ cp, const int* __restrict__ cn, const int* __restrict__ rp,
                             const int* __restrict__ rn, const int* __restrict__ cq, int ncols, int rows,
                             int* __restrict__ rm) {
@@ -183,7 +183,7 @@ __global__ void k_merge_csc(const int* __restrict__ cp, const int* __restrict__ 
             if (q >= q1 || (p < p1 && rp[p] <= rn[q]))
                 e = 4 * rp[p++];
             else
-                e = (int)((unsigned)(4 * rn[q++]) | 0x80000000u);
+                e = csc_neg_base(rows) + 4 * rn[q++];
             rm[csc_entry(cq, j, i++)] = e;
         }
         for (; i < n; ++i) rm[csc_entry(cq, j, i)] = 4 * rows;
@@ -206,9 +206,10 @@ __device__ inline float exact_out(const uint16_t* __restrict__ X3, int K, int ld
     const int g = j / kCscGroup, n = 4 * (cq[g + 1] - cq[g]);
     for (int i = 0; i < n; ++i) {
         const int r = rm[csc_entry(cq, j, i)];
-        const int k = (r & kCscRowMask) >> 2;
-        if (k >= K) break;  // the column's padding
-        acc = fmaf(xk(k), r < 0 ? -1.0f : 1.0f, acc);
+        if (r == 4 * K) break;  // the column's padding
+        const bool neg = r >= csc_neg_base(K);
+        const int k = (neg ? r - csc_neg_base(K) : r) >> 2;
+        acc = fmaf(xk(k), neg ? -1.0f : 1.0f, acc);
     }
     if (!BIAS_FIRST) acc += Bias[j];
     if (PRELU) acc = (acc < 0.0f) ? a * acc : acc;

@@ -2,14 +2,13 @@
 //
 // k_stream stages 256 rows of X per workgroup; with M = 1 (the reference
 // harness's first cases, main.cpp:258-261) the staging, the barriers and the
-// 256-row epilogue are all overhead: ~37 us for 1 x 512 x 2048.  For M <= 16
+// 256-row epilogue are all overhead: ~37 us for 1 x 512 x 2048.  For M <= 4
 // one LANE per output column walks the column's merged row list (the plan's
-// CSC copy, +1 and -1 rows in ascending k, -1 rows tagged in bit 31) and adds
-// +-X[m, k] in that order, straight from L1/L2 (X is at most 16 x K floats
-// here), then the bias, then the PReLU: the exact arithmetic of k_stream's
-// fast order, so the outputs are bit-identical to the gather path's (K not
-// split) and to the reference's dense.c gemm_basic (dense.c:64-77: y = 0,
-// y += X*W over ascending k, + B; a ternary W makes every product exact).
+// CSC copy, +1 and -1 rows in ascending k) and adds +-X[m, k] in that order,
+// then the bias, then the PReLU: the exact arithmetic of k_stream's fast
+// order, so the outputs are bit-identical to the gather path's (K not split)
+// and to the reference's dense.c gemm_basic (dense.c:64-77: y = 0, y += X*W
+// over ascending k, + B; a ternary W makes every product exact).
 // (Rounds 2-4 summed 64 lanes' strided partial sums and reduced them by a
 // butterfly: within the bound, not in the gather's order; the reference's
 // main.cpp checks tcsc_sgemm_basic against dense.c's gemm_basic with an
@@ -23,20 +22,29 @@ namespace {
 
 constexpr int kBlock = kCscGroup;  // columns (lanes) per workgroup: one wave, one group of the list layout
 
+// Look-ahead of the entry ring, in quads: one wave per CU here, so a lane can
+// hold 48 quads (192 VGPRs) at M = 1, enough to cover the loads' latency.
+template <int MB>
+constexpr int ring_quads() {
+    return MB == 1 ? 48 : (MB == 2 ? 32 : 8);
+}
+
 // One lane per column; the column's sum is one dependent chain of adds in
 // the merged list's order, so everything else runs off that chain:
-//  * the workgroup stages X in LDS as rows of K+1 floats, the last one -0.0
-//    (the exact additive identity): 8 loads per lane in flight, addresses
-//    clamped instead of branched around (a load under a runtime condition
-//    makes hipcc branch around it and drain vmcnt per load);
-//  * the list (csc_prepare/csc_fill: entries 4*k with the -1 sign in bit 31,
-//    the 64 columns of this workgroup interleaved by 16-B quads, padded to
-//    the group's length with 4*K entries) is read one quad per lane and load
-//    -- a coalesced 1 KiB for the wave -- 16 quads ahead of the adds, and
-//    the values 3 quads ahead, for the group's whole length (a wave-uniform
-//    trip count, a multiple of 16 quads);
-//  * an entry is directly the byte offset of its value in an LDS row
-//    (padding reads the -0.0), so an add is ds_read -> sign xor -> v_add;
+//  * the workgroup stages each row of X in LDS as the pair [X | -0.0 | 0.. |
+//    -X | 0..] (2*Kp floats, tcsc_internal.h): an entry of the list (4k, or
+//    4Kp + 4k for a -1 row, or 4K for padding) is then directly the byte
+//    offset of +-X[m, k], so an add is one ds_read and one v_add (negation is
+//    exact: acc + (-x) is the gather's fma(x, -1, acc)); the staging keeps 16
+//    16-B loads per lane in flight, addresses clamped instead of branched
+//    around (a load under a runtime condition makes hipcc branch around it
+//    and drain vmcnt per load);
+//  * the list (the 64 columns of this workgroup interleaved by 16-B quads,
+//    padded to the group's length, a multiple of 16 quads) is read one quad
+//    per lane and load -- a coalesced 1 KiB for the wave -- ring_quads()
+//    quads ahead of the adds, and the values 3 quads ahead; the ring is
+//    unrolled in phases of 16 quads so every slot is a static register set,
+//    and the sum never runs past the group;
 //  * the look-ahead loads are pinned ahead of the adds (hipcc would sink
 //    them to their first use).
 template <int MB, bool BIAS_FIRST, bool PRELU>
@@ -45,18 +53,42 @@ k_small_m(const float* __restrict__ X, int M, int K, const int* __restrict__ cq,
           int ncols, const float* __restrict__ Bias, float* __restrict__ Y, int ldy, float a) {
     extern __shared__ float xs[];
     const int lane = threadIdx.x;
+    const int Kp = csc_half(K), S = 2 * Kp;  // floats per half / per staged row pair
+    // 16-B loads, 16 per lane in flight (16 KiB per wave per round trip), where
+    // X's rows are 16-B aligned; 4-B loads otherwise
+    const bool vec = (K & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
     for (int r = 0; r < M; ++r) {
         const float* __restrict__ xr = X + (size_t)r * K;
-        float* dr = xs + r * (K + 1);
-        for (int k0 = 0; k0 < K; k0 += 8 * kBlock) {
-            float v[8];
+        float* dr = xs + (size_t)r * S;
+        if (vec) {
+            for (int k0 = 0; k0 < K; k0 += 16 * 4 * kBlock) {
+                float4 v[16];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = xr[min(k0 + u * kBlock + lane, K - 1)];
+                for (int u = 0; u < 16; ++u)
+                    v[u] = *reinterpret_cast<const float4*>(xr + min(k0 + 4 * (u * kBlock + lane), K - 4));
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (k0 + u * kBlock + lane < K) dr[k0 + u * kBlock + lane] = v[u];
+                for (int u = 0; u < 16; ++u) {
+                    const int k = k0 + 4 * (u * kBlock + lane);
+                    if (k < K) {
+                        *reinterpret_cast<float4*>(dr + k) = v[u];
+                        *reinterpret_cast<float4*>(dr + Kp + k) = make_float4(-v[u].x, -v[u].y, -v[u].z, -v[u].w);
+                    }
+                }
+            }
+        } else {
+            for (int k0 = 0; k0 < K; k0 += 8 * kBlock) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = xr[min(k0 + u * kBlock + lane, K - 1)];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (k0 + u * kBlock + lane < K) {
+                        dr[k0 + u * kBlock + lane] = v[u];
+                        dr[Kp + k0 + u * kBlock + lane] = -v[u];
+                    }
+            }
         }
-        if (lane == 0) dr[K] = -0.0f;
+        if (lane == 0) dr[K] = -0.0f;  // what padding entries read: the exact additive identity
     }
     __syncthreads();
     const int j = blockIdx.x * kBlock + lane;
@@ -65,21 +97,19 @@ k_small_m(const float* __restrict__ X, int M, int K, const int* __restrict__ cq,
     float acc[MB];
 #pragma unroll
     for (int r = 0; r < MB; ++r) acc[r] = BIAS_FIRST ? b : 0.0f;
-    const int q0 = cq[blockIdx.x], nq = cq[blockIdx.x + 1] - q0;  // uniform; a multiple of 4
+    const int q0 = cq[blockIdx.x], nq = cq[blockIdx.x + 1] - q0;  // uniform; a multiple of 16
     const int4* __restrict__ lst = reinterpret_cast<const int4*>(rm) + (size_t)q0 * kBlock + lane;
-    // one (entry, row) value with the entry's sign applied (rows >= M read row M-1's, unused)
+    const char* xb = reinterpret_cast<const char*>(xs);  // row pair r at byte r * S * 4
+    // +-X[r, k] for an entry (rows >= M read row M-1's, unused)
     auto xval = [&](int e, int r) {
         const int rr = r < M ? r : M - 1;
-        const float v = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(xs) + (e & kCscRowMask) +
-                                                         rr * (K + 1) * 4);
-        return __builtin_bit_cast(float, __builtin_bit_cast(unsigned, v) ^ ((unsigned)e & 0x80000000u));
+        return *reinterpret_cast<const float*>(xb + e + rr * S * 4);
     };
-    // Look-ahead: entries kIR quads ahead (index ring, refilled by coalesced
-    // loads), values kXD quads ahead (value ring, LDS reads); the body is
-    // unrolled by kIR so every slot is a static register set.  Group lengths
-    // are multiples of kIR quads; the guard quads past the last group are 0.
-    constexpr int kIR = MB <= 2 ? 16 : 8, kXR = 4, kXD = 3;  // MB = 4: 8 quads keep it under 256 VGPRs
-    static_assert(kIR % kXR == 0 && 16 % kIR == 0 && kXD < kXR && kIR <= kCscGuardQuads, "look-ahead geometry");
+    // entries kIR quads ahead (index ring, refilled by coalesced loads), values
+    // kXD quads ahead (value ring, LDS reads); phases of kPh quads
+    constexpr int kIR = ring_quads<MB>(), kPh = kIR < 16 ? kIR : 16, kXR = 4, kXD = 3;
+    static_assert(kIR % kPh == 0 && 16 % kPh == 0 && kPh % kXR == 0 && kXD < kXR && kIR <= kCscGuardQuads,
+                  "look-ahead geometry");
     int4 ring[kIR];
 #pragma unroll
     for (int i = 0; i < kIR; ++i) ring[i] = lst[(size_t)i * kBlock];
@@ -95,19 +125,23 @@ k_small_m(const float* __restrict__ X, int M, int K, const int* __restrict__ cq,
     };
 #pragma unroll
     for (int i = 0; i < kXD; ++i) load_x(ring[i], xv[i]);
-    for (int q0 = 0; q0 < nq; q0 += kIR) {
+    for (int qb = 0; qb < nq; qb += kIR) {
 #pragma unroll
-        for (int s = 0; s < kIR; ++s) {
-            // values of quad q + kXD (its entries arrived kIR - kXD steps ago)
-            load_x(ring[(s + kXD) % kIR], xv[(s + kXD) % kXR]);
-            ring[s] = lst[(size_t)(q0 + s + kIR) * kBlock];  // quad q + kIR into the slot quad q left
-            asm volatile("" ::: "memory");  // the look-ahead loads stay ahead of the adds
-            // acc + x with x = +-X[m, k] (sign applied exactly) is fma(X, +-1, acc):
-            // the gather's arithmetic; padding adds -0.0, which changes nothing
+        for (int ph = 0; ph < kIR / kPh; ++ph) {
+            if (ph > 0 && qb + ph * kPh >= nq) break;  // uniform: the group ends on a 16-quad boundary
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int s = 0; s < kPh; ++s) {
+                const int t = ph * kPh + s;  // compile-time after unrolling
+                // values of quad q + kXD (its entries arrived kIR - kXD steps ago)
+                load_x(ring[(t + kXD) % kIR], xv[(t + kXD) % kXR]);
+                ring[t] = lst[(size_t)(qb + t + kIR) * kBlock];  // quad q + kIR into the slot quad q left
+                asm volatile("" ::: "memory");  // the look-ahead loads stay ahead of the adds
+                // padding adds -0.0, which changes nothing
 #pragma unroll
-                for (int r = 0; r < MB; ++r) acc[r] = acc[r] + xv[s % kXR][i][r];
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int r = 0; r < MB; ++r) acc[r] = acc[r] + xv[t % kXR][i][r];
+            }
         }
     }
     if (!col_ok) return;
@@ -130,8 +164,8 @@ void launch_one(const float* X, int M, int K, const int* cq, const int* rm, int 
     }();
     (void)attr;
     const dim3 grid((ncols + kBlock - 1) / kBlock), block(kBlock);
-    hipLaunchKernelGGL((k_small_m<MB, BF, PR>), grid, block, (size_t)M * (K + 1) * sizeof(float), st, X, M, K, cq,
-                       rm, ncols, B, Y, ldy, a);
+    hipLaunchKernelGGL((k_small_m<MB, BF, PR>), grid, block, small_m_lds_bytes(M, K), st, X, M, K, cq, rm, ncols, B,
+                       Y, ldy, a);
 }
 
 template <int MB>
