@@ -112,3 +112,38 @@ def test_specials_and_off_switch(gpu, oracle, monkeypatch):
     Y64, S64 = oracle.f64_rows(Xf, Wref, B)
     assert pyoracle.check_close(run(W, Xf, B, "basic"), Y64, S64)[0]
     W.free()
+
+
+@pytest.mark.parametrize("K", [1, 5, 4093, 4096])
+def test_ragged_k_and_unaligned_x_equal_gather(gpu, oracle, monkeypatch, K):
+    """The staging's two forms -- 16-B loads where K % 4 == 0 and X is 16-B
+    aligned, 4-B loads otherwise (K = 1, 5, 4093, or X one float off a 16-B
+    boundary) -- and the row pair's padding (Kp = K + 1 rounded up to 4): bit
+    for bit the gather's fast order with K unsplit."""
+    import torch
+
+    dev = torch.device("cuda:0")
+    M, N = 2, 200
+    Wd = oracle.ternary((K, N), 0.3, 1000 + K)
+    X, B = oracle.uniform((M, K), 1100 + K), oracle.uniform((N,), 1200 + K)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    plan = tcsc_amd.Plan(W, 0, N)
+    assert plan.launch_info(M)[0] == "small"
+    dB = torch.from_numpy(B).to(dev)
+    backing = torch.zeros(M * K + 1, device=dev)
+    for shift in (0, 1):  # shift 1: X starts 4 B past a 16-B boundary
+        dX = backing[shift:shift + M * K].view(M, K)
+        dX.copy_(torch.from_numpy(X).to(dev))
+        ys = {}
+        for small in ("4", "0"):
+            monkeypatch.setenv("TCSC_SMALL_M", small)
+            monkeypatch.setenv("TCSC_SLICES", "1")
+            monkeypatch.setenv("TCSC_PATH", "gather")
+            dY = torch.full((M, N), float("nan"), device=dev)
+            plan.sgemm(dX, dB, dY, M, N, "prelu_basic", 0.2)
+            torch.cuda.synchronize()
+            ys[small] = dY.cpu().numpy()
+        np.testing.assert_array_equal(ys["4"].view(np.uint32), ys["0"].view(np.uint32),
+                                      err_msg=f"K={K} shift={shift}")
+    plan.destroy()
+    W.free()
