@@ -845,7 +845,8 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     // and the partner's slab, in slice order -- k_reduce4's adds, the same
     // bits.  The first finisher never waits, so no residency is assumed.
     const bool own_lds = OUT == 2 && gridDim.z == 4;  // combine_tile: the own band stays in the LDS
-    int pair_role = 0;  // OUT 3: 0 = store the slab, 1 = combine
+    int pair_role = 0;  // OUT 3: 0 = the tile's first slice to finish, 1 = the second
+    const bool pair_split = OUT == 3 && (combine_giveup & 2);  // OUT 3: split halves (resident grid)
     unsigned* const pw = OUT == 3 ? ccnt + (size_t)(t.rt * (int)gridDim.x + t.cb) * kCombineWords : nullptr;
     auto epilogue = [&](auto how_) {
         constexpr int HOW = decltype(how_)::value;
@@ -854,7 +855,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
             int* role = reinterpret_cast<int*>(lds + kLdsBytes - 16);
             if (threadIdx.x == 0) {
                 int r = __hip_atomic_fetch_add(pw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u ? 0 : 1;
-                if (r == 1) {
+                if (r == 1 && !pair_split) {
                     // the partner has arrived, so it is running and will publish: the bound
                     // (100 ms) only keeps a broken launch from hanging the device
                     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -891,8 +892,10 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
             bq.z = col + 2 < col_end ? Bias[col + 2] : 0.f;
             bq.w = col + 3 < col_end ? Bias[col + 3] : 0.f;
         }
-#pragma unroll
-        for (int h = 0; h < 256 / kEpiRows; ++h) {
+        // one pass: park rows [64 h, 64 h + 64) of the tile, then store them (OUT 3:
+        // fin = finalize Y from this slice's partial and the partner's slab,
+        // else store the partial to this slice's slab); no trailing barrier
+        auto pass = [&](const int h, const bool fin) {
             if (active && lane / kLanesPerPass == h) {
                 const int lh = lane % kLanesPerPass;
 #pragma unroll
@@ -943,7 +946,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                         if constexpr (OUT == 3) {
                             // vec_ok and whole quads (the launcher's conditions)
                             const int off = (int)(((size_t)t.z * M + row) * ncols + col) * 4;
-                            if (pair_role == 0) {
+                            if (!fin) {
                                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), slab_rs, off, 0,
                                                                        kSc1);
                             } else {
@@ -1018,7 +1021,98 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                     }
                 }
             }
-            if (h + 1 < 256 / kEpiRows) __syncthreads();  // region reused by the next pass
+        };
+        if (!pair_split) {
+#pragma unroll
+            for (int h = 0; h < 256 / kEpiRows; ++h) {
+                pass(h, OUT == 3 && pair_role == 1);
+                if (h + 1 < 256 / kEpiRows) __syncthreads();  // region reused by the next pass
+            }
+            if (OUT == 3 && pair_role == 0) {  // publish the slab: every wave's sc1 stores drained, then one agent add
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (threadIdx.x == 0) __hip_atomic_fetch_add(pw + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else if constexpr (OUT == 3) {
+            // Split pairwise (the grid is resident; DESIGN.md §4 k_reduce): the first
+            // finisher F stores rows 0..127 of its partial, the second S rows 128..255;
+            // each then finalizes the half the other stored, from its registers and
+            // the partner's slab.  Words: pw[0] arrival, pw[1] F's half ready, pw[2]
+            // who finalizes rows 128..255 (2: S stored its half, F finalizes; 1: F
+            // gave up waiting, stored that half too, S finalizes), pw[3] done.
+            int* dec = reinterpret_cast<int*>(lds + kLdsBytes - 16) + 1;
+            const bool first = pair_role == 0;
+            const int own = first ? 0 : 2;  // passes of the half this slice stores
+            pass(own, false);
+            __syncthreads();
+            pass(own + 1, false);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores have left
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                int d;
+                if (first) {
+                    __hip_atomic_fetch_add(pw + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    unsigned v = 0;
+                    if (!(combine_giveup & 1)) {  // the partner may not be resident: a bounded wait
+                        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                        while ((v = __hip_atomic_load(pw + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u &&
+                               __builtin_amdgcn_s_memrealtime() - t0 < kCombineWaitTicks)
+                            __builtin_amdgcn_s_sleep(2);
+                    }
+                    d = v == 2u ? 1 : 0;  // 1: finalize rows 128..255; 0: gave up
+                } else {
+                    unsigned expect = 0u;
+                    const bool mine = __hip_atomic_compare_exchange_strong(
+                        pw + 2, &expect, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    d = mine ? 0 : 1;  // 1: F gave up and stored rows 128..255 as well
+                    // F has arrived, so it is running and publishes its half without
+                    // waiting; the bound (100 ms) only keeps a broken launch from hanging
+                    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                    while (__hip_atomic_load(pw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+                           __builtin_amdgcn_s_memrealtime() - t0 < 10000000ull)
+                        __builtin_amdgcn_s_sleep(2);
+                }
+                dec[0] = d;
+            }
+            __syncthreads();
+            const int d = __builtin_amdgcn_readfirstlane(dec[0]);
+            if (first) {
+                if (d == 0) {  // give the second half up: store it, then try to hand it over
+                    pass(2, false);
+                    __syncthreads();
+                    pass(3, false);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                    if (threadIdx.x == 0) {
+                        unsigned expect = 0u;
+                        dec[0] = __hip_atomic_compare_exchange_strong(pw + 2, &expect, 1u, __ATOMIC_RELAXED,
+                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     ? 0
+                                     : 1;  // 1: S stored its half in the meantime, so finalize it here
+                    }
+                    __syncthreads();
+                }
+                if (__builtin_amdgcn_readfirstlane(dec[0]) == 1) {
+                    pass(2, true);
+                    __syncthreads();
+                    pass(3, true);
+                }
+            } else {
+                pass(0, true);
+                __syncthreads();
+                pass(1, true);
+                if (d == 1) {
+                    __syncthreads();
+                    pass(2, true);
+                    __syncthreads();
+                    pass(3, true);
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0 &&
+                __hip_atomic_fetch_add(pw + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) {
+                for (int i = 0; i < 4; ++i) __hip_atomic_store(pw + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     };
 
@@ -1030,13 +1124,6 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
 #endif
         if constexpr (OUT == 2) combine_tile<BIAS_FIRST, PRELU>(ws, M, ncols, Bias, Y, ldy, a, ccnt, t, lds, combine_giveup,
                                                          own_lds);
-        if constexpr (OUT == 3) {
-            if (pair_role == 0) {  // publish the slab: every wave's sc1 stores drained, then one agent add
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (threadIdx.x == 0) __hip_atomic_fetch_add(pw + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
 #ifdef TCSC_STAMPS
         rt_[4] = rtstamp();
         if (threadIdx.x == 0) {
@@ -1460,10 +1547,12 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
                        reinterpret_cast<uintptr_t>(g.B)) & 15) == 0;
     const int cm = combine_mode(slices, (long long)grid.x * grid.y * grid.z, (long long)grid.x * grid.y, total,
                                 g.num_cus, g.ccnt != nullptr, vec);
-    if (cm == 3) {  // pairwise: no residency needed
+    if (cm == 3) {  // pairwise: no residency needed; the split halves where the grid is resident
+        const long long wgs = (long long)grid.x * grid.y * grid.z;
+        const int split = (g.num_cus > 0 && wgs <= g.num_cus && env_int("TCSC_PAIR_SPLIT", 1) != 0) ? 2 : 0;
         hipLaunchKernelGGL((k_stream<BF, PR, 3, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
                            g.n_entries, g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a,
-                           g.ws, pfd, pfl, g.ccnt, 0);
+                           g.ws, pfd, pfl, g.ccnt, split | (g.combine_giveup & 1));
         return hipGetLastError();
     }
     if (cm == 2) {  // row bands: every workgroup of the grid resident at once (one per CU)
