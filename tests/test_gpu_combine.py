@@ -1,5 +1,6 @@
 """The in-launch split-K combines (k_stream OUT 2, `combine_tile`, by row
-bands; OUT 3, pairwise, at 2 slices; DESIGN.md §4 k_reduce; TCSC_COMBINE=1)
+bands; OUT 3, pairwise at 2 slices -- split halves on resident grids, the
+classic form on larger ones; DESIGN.md §4 k_reduce; TCSC_COMBINE=1)
 against the k_stream + k_reduce4 pair
 (TCSC_COMBINE=0): the same adds in the same order per element, so the outputs
 must be bit-identical -- on cfg 2/3, on ragged shapes (M not a multiple of
