@@ -988,21 +988,9 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                                 static_assert(kEpiRows == 64, "a pass is one band at Z = 4");
                                 *reinterpret_cast<float4*>(lds + kOwnBandOff + R * kRowBytes +
                                                            (col - t.cb * kWgCols) * 4) = v;
-                            } else if (vec_ok && col + 3 < col_end) {
+                            } else {  // whole quads: the launcher combines in launch only when ncols % 4 == 0
                                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), slab_rs, off, 0,
                                                                        kSc1);
-                            } else {
-                                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v.x), slab_rs, off, 0,
-                                                                      kSc1);
-                                if (col + 1 < col_end)
-                                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v.y), slab_rs,
-                                                                          off + 4, 0, kSc1);
-                                if (col + 2 < col_end)
-                                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v.z), slab_rs,
-                                                                          off + 8, 0, kSc1);
-                                if (col + 3 < col_end)
-                                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v.w), slab_rs,
-                                                                          off + 12, 0, kSc1);
                             }
                         } else if (vec_ok && col + 3 < col_end) {
                             if (OUT == 0 && HOW != 1) {  // Y is never re-read here: keep it out of L2's way
