@@ -128,6 +128,9 @@ int tcsc_gpu_launch_info(const tcsc_gpu_plan *plan, int M, int *path, int *slice
 /* For TCSC_PATH_GATHER with a K split, where the split-K slabs are combined
  * (N % 4 == 0 and the plan's reserved workspace needed for either in-launch
  * form; TCSC_COMBINE=0 turns both off, =1 lifts the band form's size rule):
+ *   4  inside the k_stream launch, pairwise in split halves (exactly 2
+ *      slices, the grid fits the chip at one workgroup per CU: each slice
+ *      stores half its partial and finalizes the other half)
  *   3  inside the k_stream launch, pairwise (exactly 2 slices: the tile's
  *      first slice to finish stores its slab, the second combines; any grid)
  *   2  inside the k_stream launch, by row bands (>= 3 slices, the grid fits

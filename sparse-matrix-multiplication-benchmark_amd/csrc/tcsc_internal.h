@@ -211,7 +211,8 @@ hipError_t plan_fill(const PlanDev& in, PlanOut& out, hipStream_t st);      // -
 int choose_slices(int M, int ncols, int K, long long nnz, int n_groups, size_t ws_bytes, int force);
 // where the split-K slabs of a gather launch are combined: 0 by k_reduce4
 // after it, 2 inside k_stream by row bands (combine_tile: >= 3 slices, the
-// grid resident at once), 3 inside k_stream pairwise (exactly 2 slices)
+// grid resident at once), 3 inside k_stream pairwise (exactly 2 slices), 4
+// pairwise in split halves (2 slices, the grid resident at once)
 int combine_mode(int slices, long long wgs, long long tiles, long long slab_floats, int num_cus, bool have_words,
                  bool vec);
 int normalized_slices(int K, int slices);  // the K split launch_gemm actually runs

@@ -1474,7 +1474,9 @@ void pf_stream_params(long long n_entries, int n_groups, int n_chunks, int* dist
 // Split-K slabs combined inside the k_stream launch or by k_reduce4 after it.
 //  * 2 slices: pairwise (k_stream OUT 3): the tile's first slice to finish
 //    stores its slab, the second combines -- no reduce launch, half the slab
-//    bytes, and no wait on a workgroup that has not started, so any grid.
+//    bytes, and no wait on a workgroup that has not started, so any grid (3);
+//    where the grid is resident each slice stores one half and finalizes the
+//    other (4, the split halves; TCSC_PAIR_SPLIT=0 keeps 3).
 //  * 3 or more: row bands (combine_tile, OUT 2) where the whole grid is
 //    resident (one workgroup per CU), from 64 workgroups on (measured: cfg
 //    2/3 at 4 slices 79 -> 74 us; cfg 1's 6 workgroups 23 -> 27 us: the
@@ -1488,7 +1490,8 @@ int combine_mode(int slices, long long wgs, long long tiles, long long slab_floa
         return 0;
     const int c = env_int("TCSC_COMBINE", -1);
     if (c == 0) return 0;
-    if (slices == 2 && (c != 2 || num_cus <= 0 || wgs > num_cus)) return 3;
+    if (slices == 2 && (c != 2 || num_cus <= 0 || wgs > num_cus))  // pairwise: split halves on a resident grid
+        return (num_cus > 0 && wgs <= num_cus && env_int("TCSC_PAIR_SPLIT", 1) != 0) ? 4 : 3;
     if (num_cus <= 0 || wgs > num_cus) return 0;
     return (c > 0 || wgs >= 64) ? 2 : 0;
 }
@@ -1535,9 +1538,8 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
                        reinterpret_cast<uintptr_t>(g.B)) & 15) == 0;
     const int cm = combine_mode(slices, (long long)grid.x * grid.y * grid.z, (long long)grid.x * grid.y, total,
                                 g.num_cus, g.ccnt != nullptr, vec);
-    if (cm == 3) {  // pairwise: no residency needed; the split halves where the grid is resident
-        const long long wgs = (long long)grid.x * grid.y * grid.z;
-        const int split = (g.num_cus > 0 && wgs <= g.num_cus && env_int("TCSC_PAIR_SPLIT", 1) != 0) ? 2 : 0;
+    if (cm == 3 || cm == 4) {  // pairwise: no residency needed (3); the split halves on a resident grid (4)
+        const int split = cm == 4 ? 2 : 0;
         hipLaunchKernelGGL((k_stream<BF, PR, 3, 0>), grid, block, 0, st, g.XT, ldxt, g.M, g.K, g.ent, g.sptr,
                            g.n_entries, g.ent, g.sptr, g.n_entries, g.n_groups, g.ncols, nch, cps, g.B, g.Y, g.ldy, g.a,
                            g.ws, pfd, pfl, g.ccnt, split | (g.combine_giveup & 1));

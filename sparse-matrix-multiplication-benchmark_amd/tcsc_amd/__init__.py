@@ -463,11 +463,12 @@ class Plan:
 
     def combine_mode(self, M: int):
         """How a gather launch of M rows combines its split-K slabs: 'pairwise'
-        (2 slices, inside k_stream), 'bands' (>= 3 slices, inside k_stream) or
-        None (k_reduce4 after it, or no split) -- tcsc_gpu_launch_combine."""
+        (2 slices, inside k_stream, any grid), 'pairwise-split' (2 slices, split
+        halves, a resident grid), 'bands' (>= 3 slices, inside k_stream) or None
+        (k_reduce4 after it, or no split) -- tcsc_gpu_launch_combine."""
         v = C.c_int()
         _check(lib().tcsc_gpu_launch_combine(self.handle, int(M), C.byref(v)), "tcsc_gpu_launch_combine")
-        return {2: "bands", 3: "pairwise"}.get(v.value)
+        return {2: "bands", 3: "pairwise", 4: "pairwise-split"}.get(v.value)
 
     def reserve(self, max_M: int) -> None:
         """Allocate the workspace (X^T + split-K slabs) for launches of up to max_M rows."""

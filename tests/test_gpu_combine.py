@@ -112,15 +112,24 @@ def test_combine_integer_exact(gpu, oracle, monkeypatch):
     plan.destroy()
 
 
-def test_combine_graph_replay_with_new_x(gpu, monkeypatch):
+@pytest.mark.parametrize("M,K,N,slices,split,expect", [
+    (1024, 4096, 4096, None, None, "bands"),     # cfg 2: row bands, own band in the LDS
+    (1024, 8192, 2048, "2", None, "pairwise-split"),  # 64 workgroups, resident: split halves
+    (1024, 8192, 2048, "2", "0", "pairwise"),         # the same in the classic form
+])
+def test_combine_graph_replay_with_new_x(gpu, monkeypatch, M, K, N, slices, split, expect):
     """A captured split-K launch with the in-launch combine, replayed with new
     X in place: each replay must find the tile words at zero."""
     import torch
 
     monkeypatch.setenv("TCSC_COMBINE", "1")
-    M, K, N = 1024, 4096, 4096
+    if slices:
+        monkeypatch.setenv("TCSC_SLICES", slices)
+    if split:
+        monkeypatch.setenv("TCSC_PAIR_SPLIT", split)
     plan, _ = _plan(torch, K, N, 0.05, 9)
     plan.reserve(M)
+    assert plan.combine_mode(M) == expect
     dev = torch.device("cuda:0")
     X = torch.empty((M, K), device=dev)
     B = torch.rand((N,), device=dev) * 2 - 1
@@ -151,6 +160,7 @@ def test_combine_graph_replay_with_new_x(gpu, monkeypatch):
     (1024, 4096, 4096, 0.05, "0", None),          # switched off
     (128, 256, 256, 0.1, None, None),             # cfg 1: 6 workgroups, k_reduce4 is cheaper
     (128, 256, 256, 0.1, "1", "bands"),           # forced
+    (4096, 16384, 2048, 0.02, None, "pairwise-split"),  # the 8-way column block: 256 workgroups, resident
     (2048, 4096, 8192, 0.05, None, "pairwise"),   # 2 slices x 256 tiles: the grid exceeds the chip, pairs need no residency
     (2048, 4096, 8192, 0.05, "0", None),
 ])
@@ -163,6 +173,8 @@ def test_launch_combine_reports_the_path(gpu, monkeypatch, M, K, N, density, env
         monkeypatch.setenv("TCSC_COMBINE", env)
     if M == 2048:
         monkeypatch.setenv("TCSC_SLICES", "2")
+    else:
+        monkeypatch.delenv("TCSC_SLICES", raising=False)
     plan, _ = _plan(torch, K, N, density, 1)
     plan.reserve(M)
     path, slices = plan.launch_info(M)
@@ -192,7 +204,7 @@ def test_combine_give_up_path_bit_identical(gpu, monkeypatch, M, K, N, density, 
     plan, _ = _plan(torch, K, N, density, 31 + M)
     plan.reserve(M)
     monkeypatch.setenv("TCSC_COMBINE", "1")
-    assert plan.combine_mode(M) == ("pairwise" if slices == "2" else "bands")
+    assert plan.combine_mode(M) == ("pairwise-split" if slices == "2" else "bands")
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)
     g.manual_seed(77 + K)
