@@ -688,7 +688,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     const int c_end = min(nch, c_begin + chunks_per_slice);
     const bool active = g < G;
 #ifdef TCSC_STAMPS
-    unsigned long long rt_[5] = {rtstamp(), 0, 0, 0, 0};
+    unsigned long long rt_[7] = {rtstamp(), 0, 0, 0, 0, 0, 0};  // + [5] loads drained, [6] epilogue barrier
 #endif
 
     facc_t acc[TCSC_ACC_VECS];
@@ -824,6 +824,9 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         // no LDS-DMA may still be writing when the workgroup's LDS is
         // released, and the last (unused) stream load must have landed
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#ifdef TCSC_STAMPS
+        rt_[5] = rtstamp();
+#endif
     };
 
     // Epilogue: lanes hold rows (4 per lane), so a direct store would put
@@ -851,6 +854,9 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     auto epilogue = [&](auto how_) {
         constexpr int HOW = decltype(how_)::value;
         __syncthreads();  // every wave is done with the tile ring
+#ifdef TCSC_STAMPS
+        rt_[6] = rtstamp();
+#endif
         if constexpr (OUT == 3) {
             int* role = reinterpret_cast<int*>(lds + kLdsBytes - 16);
             if (threadIdx.x == 0) {
@@ -1117,7 +1123,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
         if (threadIdx.x == 0) {
             const int wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
             if (wg < kStampWgs)
-                for (int i = 0; i < 5; ++i) g_wgtime[wg * 8 + i] = rt_[i];
+                for (int i = 0; i < 7; ++i) g_wgtime[wg * 8 + i] = rt_[i];
         }
 #endif
     } else if constexpr (ORDER == 1) {

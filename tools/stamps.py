@@ -87,7 +87,7 @@ try:
     L.tcsc_debug_wgtimes.argtypes = [C.c_void_p, C.c_size_t]
     tb = np.zeros(n_wg * 8, np.uint64)
     assert L.tcsc_debug_wgtimes(tb.ctypes.data, tb.nbytes) == 0
-    t = tb.reshape(n_wg, 8)[:, :5].astype(np.float64)
+    t = tb.reshape(n_wg, 8)[:, :7].astype(np.float64)
     t = t[t[:, 0] > 0]
     t0 = t[:, 0].min()
     us = (t - t0) / 100.0  # 100 MHz ticks -> us
@@ -97,6 +97,10 @@ try:
     print(f"  prologue   : mean {pro.mean():7.2f}  max {pro.max():7.2f}   (entry -> chunk loop)")
     print(f"  chunk loop : mean {loop.mean():7.2f}  min {loop.min():7.2f}  max {loop.max():7.2f}")
     print(f"  epilogue   : mean {epi.mean():7.2f}  max {epi.max():7.2f}   (LDS transpose + Y/slab stores issued)")
+    if (t[:, 5] > 0).all() and (t[:, 6] > 0).all():
+        drain, bar = (us[:, 5] - us[:, 2]), (us[:, 6] - us[:, 5])
+        print(f"    of which : loads drained {drain.mean():6.2f} (max {drain.max():6.2f}), "
+              f"first barrier {bar.mean():6.2f} (max {bar.max():6.2f}), passes {(epi - drain - bar).mean():6.2f}")
     print(f"  combine    : mean {comb.mean():7.2f}  max {comb.max():7.2f}")
     print(f"  end        : first {us[:, 4].min():7.2f}, last {us[:, 4].max():7.2f}, median {np.median(us[:, 4]):7.2f}")
 except (AttributeError, AssertionError) as e:
