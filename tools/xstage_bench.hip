@@ -9,6 +9,16 @@
 //          instructions per chunk, spread over all 16 waves (3 k x 4 row
 //          groups each), one M0 write per k.
 //   mode 2: as 1, issued by the 4 oldest waves only (12 k x 4 each).
+//   mode 3 (round 3's direct staging, commit 19e8dbb): every wave loads 3
+//          16-B pieces of row-major X per chunk into VGPRs (lane pair = 32 B
+//          of a row, 32 rows per instruction) two chunks ahead, and writes
+//          the previous set transposed into a ring of 2 (4 ds_write_b32 per
+//          piece, paired as ds_write2st64).
+//
+// Workgroups are mapped XCD-aware as in k_stream (--xcd 1, the default):
+// launch order L goes to XCD L % 8, and each XCD takes a contiguous range of
+// (row tile, column block, slice) items, so the workgroups of a row tile
+// share one L2.
 //
 // Geometry as k_stream: one workgroup of 16 waves per CU, 256 rows, ring of
 // 3 x (48 + 1) rows, two chunks in flight, counted vmcnt + s_barrier per
@@ -26,12 +36,22 @@ constexpr int kTK = 48, kTM = 256, kNBuf = 3, kBufRows = kTK + 1, kRow = kTM * 4
 constexpr int kLds = kNBuf * kBufRows * kRow;
 
 template <int MODE>
-__global__ void __launch_bounds__(1024, 4) stage(const float* __restrict__ X, const float* __restrict__ XT, int M,
-                                                  int K, int ldxt, int nch, int cps, float* __restrict__ dump) {
+__global__ void __launch_bounds__(1024, 4) stage(const float* X, const float* __restrict__ XT, int M, int K, int ldxt,
+                                                  int nch, int cps, float* __restrict__ dump, int xcd) {
     __shared__ __attribute__((aligned(16))) char lds[kLds];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int rt = blockIdx.y, z = blockIdx.z;
+    int cb = blockIdx.x, rt = blockIdx.y, z = blockIdx.z;
+    if (xcd) {  // item i = (rt * ncb + cb) * nz + z, dealt in contiguous ranges per XCD
+        const int n = gridDim.x * gridDim.y * gridDim.z;
+        const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        const int per = n / 8;
+        const int i = (n % 8 == 0) ? (L % 8) * per + L / 8 : L;
+        z = i % gridDim.z;
+        cb = (i / gridDim.z) % gridDim.x;
+        rt = i / (gridDim.z * gridDim.x);
+    }
+    (void)cb;
     const int m0 = rt * kTM;
     const int c0 = z * cps, c1 = min(nch, c0 + cps);
     const unsigned ldsb = (unsigned)reinterpret_cast<uintptr_t>(lds);
@@ -43,6 +63,57 @@ __global__ void __launch_bounds__(1024, 4) stage(const float* __restrict__ X, co
     for (int j = 0; j < 4; ++j) {
         const int m = min(m0 + 64 * j + lane, M - 1);
         voffB[j] = (unsigned)((size_t)(m - m0) * K * 4) - 256u * j;
+    }
+    // mode 3: lane's row and first k inside the chunk (piece 0), LDS offset in buffer 0
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    const int r3 = 32 * (wave & 7) + (lane >> 1), k3 = 8 * (wave >> 3) + 4 * (lane & 1);
+    const int rows3 = min(kTM, M - m0);
+    const __amdgpu_buffer_rsrc_t rs3 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X + (size_t)m0 * K), (short)0,
+                                                                         (int)((unsigned)rows3 * (unsigned)K * 4u),
+                                                                         0x00020000);
+    const unsigned voff3 = (unsigned)(r3 * K + k3) * 4u;
+    const unsigned lds3 = (unsigned)(k3 * kRow + 4 * r3);
+    auto load3 = [&](u32x4_t (&v)[3], int c) {
+        const unsigned base = voff3 + (unsigned)(c * kTK * 4);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) v[q] = __builtin_amdgcn_raw_buffer_load_b128(rs3, base + 64u * q, 0, 0);
+    };
+    auto write3 = [&](const u32x4_t (&v)[3], int buf) {
+        char* p = lds + lds3 + buf * (kBufRows * kRow);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) *reinterpret_cast<unsigned*>(p + (16 * q + j) * kRow) = v[q][j];
+    };
+    if constexpr (MODE == 3) {
+        float acc = 0.f;
+        if (c0 < c1) {
+            u32x4_t va[3], vb[3];
+            load3(va, c0);
+            load3(vb, c0 + 1);
+            write3(va, c0 & 1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            auto chunk = [&](int c, u32x4_t(&now)[3], u32x4_t(&nxt)[3]) {
+                __builtin_amdgcn_s_barrier();
+                load3(now, c + 2);
+                asm volatile("" ::: "memory");
+                acc += reinterpret_cast<const float*>(lds + (c & 1) * kBufRows * kRow)[threadIdx.x];
+                if (dump && c == c0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && !xcd)
+                    for (int i = threadIdx.x; i < kTK * kTM; i += 1024)
+                        dump[i] = reinterpret_cast<const float*>(lds + (c & 1) * kBufRows * kRow)[i];
+                if (c + 1 < c1) write3(nxt, (c + 1) & 1);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            };
+            int c = c0;
+            for (; c + 1 < c1; c += 2) {
+                chunk(c, va, vb);
+                chunk(c + 1, vb, va);
+            }
+            if (c < c1) chunk(c, va, vb);
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        }
+        if (acc == 12345.f && dump) dump[0] = acc;
+        return;
     }
     auto issue = [&](int c) {
         const int buf = c % kNBuf;
@@ -106,7 +177,7 @@ __global__ void __launch_bounds__(1024, 4) stage(const float* __restrict__ X, co
         if (c + 2 < c1) issue(c + 2);
         // a token read so the buffer is "used"
         acc += reinterpret_cast<const float*>(lds + (c % kNBuf) * kBufRows * kRow)[threadIdx.x];
-        if (dump && c == c0 && blockIdx.x == 0 && rt == 0 && z == 0) {
+        if (dump && c == c0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && !xcd) {
             for (int i = threadIdx.x; i < kTK * kTM; i += 1024)
                 dump[i] = reinterpret_cast<const float*>(lds + (c % kNBuf) * kBufRows * kRow)[i];
         }
@@ -117,7 +188,7 @@ __global__ void __launch_bounds__(1024, 4) stage(const float* __restrict__ X, co
 }
 
 int main(int argc, char** argv) {
-    int M = 4096, K = 16384, ncb = 8, z = 2, reps = 20;
+    int M = 4096, K = 16384, ncb = 8, z = 2, reps = 20, xcd = 1;
     bool check = false;
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "--M")) M = atoi(argv[++i]);
@@ -126,6 +197,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--z")) z = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--reps")) reps = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--check")) check = true;
+        else if (!strcmp(argv[i], "--xcd")) xcd = atoi(argv[++i]);
     }
     const int nrt = (M + kTM - 1) / kTM, nch = (K + kTK - 1) / kTK, cps = (nch + z - 1) / z;
     const int ldxt = nrt * kTM;
@@ -147,14 +219,16 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    printf("M=%d K=%d grid %dx%dx%d = %d WGs, %d chunks per WG\n", M, K, ncb, nrt, z, ncb * nrt * z, cps);
-    for (int mode = 0; mode < 3; ++mode) {
+    printf("M=%d K=%d grid %dx%dx%d = %d WGs, %d chunks per WG, XCD-aware order %d\n", M, K, ncb, nrt, z,
+           ncb * nrt * z, cps, xcd);
+    for (int mode = 0; mode < 4; ++mode) {
         auto launch = [&](float* d) {
-            if (mode == 0) hipLaunchKernelGGL(stage<0>, grid, dim3(1024), 0, 0, X, XT, M, K, ldxt, nch, cps, d);
-            if (mode == 1) hipLaunchKernelGGL(stage<1>, grid, dim3(1024), 0, 0, X, XT, M, K, ldxt, nch, cps, d);
-            if (mode == 2) hipLaunchKernelGGL(stage<2>, grid, dim3(1024), 0, 0, X, XT, M, K, ldxt, nch, cps, d);
+            if (mode == 0) hipLaunchKernelGGL(stage<0>, grid, dim3(1024), 0, 0, X, XT, M, K, ldxt, nch, cps, d, xcd);
+            if (mode == 1) hipLaunchKernelGGL(stage<1>, grid, dim3(1024), 0, 0, X, XT, M, K, ldxt, nch, cps, d, xcd);
+            if (mode == 2) hipLaunchKernelGGL(stage<2>, grid, dim3(1024), 0, 0, X, XT, M, K, ldxt, nch, cps, d, xcd);
+            if (mode == 3) hipLaunchKernelGGL(stage<3>, grid, dim3(1024), 0, 0, X, XT, M, K, ldxt, nch, cps, d, xcd);
         };
-        if (check) {
+        if (check && !xcd) {
             hipMemset(dump, 0, (size_t)kTK * kTM * 4);
             launch(dump);
             hipDeviceSynchronize();
