@@ -615,11 +615,6 @@ int sgemm_ws(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY
         }
         return TCSC_OK;
     }
-    if (tcsc::kXStage && p->rows >= (1 << 22)) {
-        // the direct-staging A/B build addresses a 256-row tile of X with 32-bit byte offsets
-        set_error("tcsc_gpu_sgemm: K=%d (the direct-staging build takes K < %d)", p->rows, 1 << 22);
-        return TCSC_E_ARG;
-    }
     const size_t xtb = tcsc::xt_bytes(M, p->rows);
     if (p->rows > 0 && (!ws || ws_bytes < xtb)) {
         set_error("tcsc_gpu_sgemm: workspace of %zu bytes < %zu needed for M=%d", ws ? ws_bytes : (size_t)0, xtb, M);

@@ -12,15 +12,8 @@ constexpr int kTM = 256;                 // rows per workgroup: 64 lanes x 4 row
 #ifndef TCSC_TK
 #define TCSC_TK 48
 #endif
-// X staging (A/B build, DESIGN.md §4 k_transpose): 1 = the gather kernel reads
-// row-major X itself (buffer loads into VGPRs two chunks ahead, transposed by
-// its ds_write_b32 stores into a ring of 2 chunks; no k_transpose pass); 0 =
-// k_transpose writes X^T and the kernel LDS-DMAs its rows (the product).
-#ifndef TCSC_XSTAGE
-#define TCSC_XSTAGE 0
-#endif
 #ifndef TCSC_NBUF
-#define TCSC_NBUF (TCSC_XSTAGE ? 2 : 3)
+#define TCSC_NBUF 3
 #endif
 constexpr int kTK = TCSC_TK;             // K rows per LDS chunk
 constexpr int kNBuf = TCSC_NBUF;         // LDS tile ring: chunk c in buffer c % kNBuf, kNBuf-1 chunks in flight
@@ -126,9 +119,6 @@ constexpr int kDmaWaves = TCSC_DMA_WAVES;
 constexpr bool kDmaEarly = TCSC_DMA_EARLY != 0;
 constexpr int kDmaPerWave = kTK / kDmaWaves;              // 1-KiB LDS-DMA rows per DMA wave and chunk
 static_assert(kDmaWaves <= kWaves && kTK % kDmaWaves == 0, "each DMA wave moves the same number of rows");
-constexpr bool kXStage = TCSC_XSTAGE != 0;
-static_assert(!kXStage || (kNBuf == 2 && kWaves == 16 && kTK % 16 == 0),
-              "direct X staging: ring of 2, 16 waves, chunks of whole 16-row pieces");
 static_assert(kLdsBytes <= 160 * 1024, "LDS");
 static_assert(kNBuf >= 2 && kNBuf <= 5, "ring of 2 (DMA(c+1) before gather(c)) or n >= 3 (DMA(c+n-1) after it)");
 

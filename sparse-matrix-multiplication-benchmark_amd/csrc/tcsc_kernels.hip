@@ -437,49 +437,6 @@ __device__ __forceinline__ void pf_touch(unsigned m0, unsigned voff, const char*
                  : "memory");
 }
 
-// Direct X staging (TCSC_XSTAGE=1, A/B build; round 3's commit 19e8dbb on
-// the current kernel): the kernel reads row-major X and writes the chunk's
-// X^T rows itself, so no X^T pass runs before it.  A chunk (256 rows x kTK
-// k) is kTK pieces of 32 rows x 8 k; wave w moves pieces q*16 + w (q <
-// kStg): rows 32*(w%8) .. +31, k 16q + 8*(w/8) .. +7.  Lane l owns row
-// 32*(w%8) + l/2 and 4 k (one 16-B buffer load: 32 B of a row per lane pair,
-// 32 rows per instruction) and stores them into 4 X^T rows (k * 1 KiB + 4 *
-// row; paired as ds_write2st64_b32).  The loads of chunk c+2 are issued right
-// after chunk c's barrier; after gather(c) chunk c+1's set goes to ring
-// buffer (c+1) % 2.  One buffer resource per workgroup covers its row tile:
-// rows past M read 0 (range check), k past K read the next row (never
-// gathered).
-#if TCSC_XSTAGE
-constexpr int kStg = kTK / 16;  // pieces per wave and chunk
-typedef unsigned xs_u32x4_t __attribute__((ext_vector_type(4)));
-struct XStage {
-    __amdgpu_buffer_rsrc_t rsrc;  // X rows [m0, m0 + min(256, M - m0)), K floats each
-    unsigned voff;                // bytes: lane's row * K*4 + its first k * 4 (chunk 0, piece 0)
-    unsigned lds_lane;            // LDS byte offset of the lane's first element in buffer 0
-};
-__device__ __forceinline__ void xstage_init(XStage& s, const float* X, int M, int K, int m0, int wave, int lane) {
-    const int rows = min(kTM, M - m0);  // K < 2^22 (host check): the tile's bytes fit 32 bits
-    s.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X + (size_t)m0 * K), (short)0,
-                                               (int)((unsigned)rows * (unsigned)K * 4u), 0x00020000);
-    const int r = 32 * (wave & 7) + (lane >> 1);     // row inside the tile
-    const int k = 8 * (wave >> 3) + 4 * (lane & 1);  // first k inside the chunk (piece 0)
-    s.voff = (unsigned)(r * K + k) * 4u;
-    s.lds_lane = (unsigned)(k * kRowBytes + 4 * r);
-}
-__device__ __forceinline__ void xstage_load(const XStage& s, xs_u32x4_t (&v)[kStg], int c) {
-    const unsigned base = s.voff + (unsigned)(c * kTK * 4);
-#pragma unroll
-    for (int q = 0; q < kStg; ++q) v[q] = __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, base + 64u * q, 0, 0);
-}
-__device__ __forceinline__ void xstage_write(const XStage& s, const xs_u32x4_t (&v)[kStg], char* lds, int buf) {
-    char* p = lds + s.lds_lane + buf * (kBufRows * kRowBytes);
-#pragma unroll
-    for (int q = 0; q < kStg; ++q)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) *reinterpret_cast<unsigned*>(p + (16 * q + j) * kRowBytes) = v[q][j];
-}
-#endif
-
 // XCD-aware tile order.  Workgroups are dealt round-robin over the 8 XCDs
 // (MI355X_MICROARCH.md "Workgroup dispatch"; speed only, never correctness),
 // so launch order L puts L % 8 on one XCD.  Renumber so each XCD gets a
@@ -766,48 +723,6 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     // layout v4) into acc.
     auto run_chain = [&](const int2* __restrict__ e, const int* __restrict__ sp, long long ne) {
         if (c_begin >= c_end) return;
-#if TCSC_XSTAGE
-        {
-            // XT is row-major X here (ldxt = K); see XStage.  Two register sets:
-            // chunk j's loads go to set j % 2 (relative to c_begin), issued two
-            // chunks ahead; the end of gather(c) stores chunk c+1's set into ring
-            // buffer (c+1) % 2 (the compiler's vmcnt wait leaves chunk c+2's
-            // loads in flight).  Loads past c_end are issued anyway (the buffer
-            // range check makes them harmless) so the waits stay counted.
-            XStage xs;
-            xstage_init(xs, XT, M, K, m0, wave, lane);
-            xs_u32x4_t va[kStg], vb[kStg];
-            xstage_load(xs, va, c_begin);
-            xstage_load(xs, vb, c_begin + 1);
-            unsigned long long cur =
-                reinterpret_cast<unsigned long long>(e + (active ? (long long)sp[(long long)g * nch + c_begin] : ne));
-            i32x16 sb[TCSC_SBUF_VECS];
-            sbuf_tail_t sbt;
-            load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
-            xstage_write(xs, va, lds, c_begin & 1);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // pad rows, chunk c_begin's rows
-            const unsigned mask = 0x3ffu;
-            auto chunk = [&](int c, xs_u32x4_t(&now)[kStg], xs_u32x4_t(&nxt)[kStg]) {
-                __builtin_amdgcn_s_barrier();
-                xstage_load(xs, now, c + 2);
-                asm volatile("" ::: "memory");
-                gather_stream(sb, sbt, cur, lane, mask, acc);  // leaves cur at the next chunk's header
-                if (c + 1 < c_end) xstage_write(xs, nxt, lds, (c + 1) & 1);
-                // the stores are complete before the next barrier; the stream
-                // load is issued after this wait so it need not land before it
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                load_stream(sb, sbt, reinterpret_cast<const char*>(cur));
-            };
-            int c = c_begin;
-            for (; c + 1 < c_end; c += 2) {
-                chunk(c, va, vb);
-                chunk(c + 1, vb, va);
-            }
-            if (c < c_end) chunk(c, va, vb);
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            return;
-        }
-#endif
         // Chunk c lives in ring buffer c % kNBuf (the plan baked that into
         // every entry).  Ring of 3: DMA(c+2) is issued right after gather(c),
         // so two chunks are in flight while one is consumed; per wave the
@@ -1507,7 +1422,6 @@ static inline int ldxt_of(int M) { return (M + kTM - 1) / kTM * kTM; }
 // X^T of one call: (chunks + kNBuf-1 look-ahead chunks) * kTK rows of ldxt
 // floats (rows >= K are never gathered), 256-B aligned size.
 size_t xt_bytes(int M, int K) {
-    if (kXStage) return ((size_t)M * K * sizeof(float) + 255) / 256 * 256;  // a copy of X (stage 1 / 2 only)
     const size_t rows = ((size_t)(K + kTK - 1) / kTK + kNBuf - 1) * kTK;
     const size_t b = rows * ldxt_of(M) * sizeof(float);
     return (b + 255) / 256 * 256;
@@ -1601,7 +1515,7 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
     if (g.order != 0) slices = 1;  // the reference orders walk K in order
     int cps = nch > 0 ? (nch + slices - 1) / slices : 1;
     slices = nch > 0 ? (nch + cps - 1) / cps : 1;
-    const int ldxt = kXStage ? g.K : ldxt_of(g.M);  // kXStage: g.XT is X itself
+    const int ldxt = ldxt_of(g.M);
     dim3 grid((g.n_groups + kWaves - 1) / kWaves, (g.M + kTM - 1) / kTM, slices);
     dim3 block(kWaves * 64);
     int pfd = 0, pfl = 1;
@@ -1661,19 +1575,6 @@ static hipError_t launch_t(const GemmArgs& g, int slices, hipStream_t st) {
 // workspace, ahead of the split-K slabs in g.ws).
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
     if (g.M <= 0 || g.ncols <= 0) return hipSuccess;
-    if (kXStage) {
-        // the kernel reads X itself: stage 1 keeps a copy of X in the
-        // workspace, stage 2 gathers from that copy, stage 0 from X
-        GemmArgs h = g;
-        if (g.K > 0 && g.stage == 1) {
-            if (!g.XT) return hipErrorInvalidValue;
-            return hipMemcpyAsync(g.XT, g.X, (size_t)g.M * g.K * sizeof(float), hipMemcpyDeviceToDevice, st);
-        }
-        h.XT = const_cast<float*>(g.stage == 2 ? g.XT : g.X);
-        const int s = choose_slices(h.M, h.ncols, h.K, h.nnz, h.n_groups, h.ws ? h.ws_bytes : 0, h.force_slices);
-        if (h.bias_first) return h.prelu ? launch_t<true, true>(h, s, st) : launch_t<true, false>(h, s, st);
-        return h.prelu ? launch_t<false, true>(h, s, st) : launch_t<false, false>(h, s, st);
-    }
     if (g.K > 0 && g.stage != 2) {
         if (!g.XT) return hipErrorInvalidValue;
         const int ldxt = ldxt_of(g.M);

@@ -122,11 +122,5 @@ lib/abl/libtcsc_amd_rnt%.so: $(SRC)/tcsc_kernels.hip $(OBJ)/tcsc_api.o $(OBJ)/tc
 	$(HIPCC) $(HIPFLAGS) -DTCSC_REDUCE_NT=$* -c $(SRC)/tcsc_kernels.hip -o $(OBJ)/abl/k_rnt$*.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)/abl/k_rnt$*.o $(OBJ)/tcsc_api.o $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o -lpthread -L$(ROCM)/lib -lrocblas -Wl,-rpath,$(ROCM)/lib
 
-# Direct X staging (A/B, DESIGN.md §4 k_transpose): lib/abl/libtcsc_amd_xs1.so -- no X^T pass, the
-# gather reads row-major X into VGPRs and transposes it into a ring of 2 (kernel and plan built
-# with the same constants).
-lib/abl/libtcsc_amd_xs%.so: $(SRC)/tcsc_kernels.hip $(SRC)/tcsc_api.cpp $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o $(HDRS) $(SRC)/gather_asm.inc
-	@mkdir -p lib/abl $(OBJ)/abl
-	$(HIPCC) $(HIPFLAGS) -DTCSC_XSTAGE=$* -c $(SRC)/tcsc_kernels.hip -o $(OBJ)/abl/k_xs$*.o
-	$(HIPCC) $(HIPFLAGS) -DTCSC_XSTAGE=$* -c $(SRC)/tcsc_api.cpp -o $(OBJ)/abl/a_xs$*.o
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)/abl/k_xs$*.o $(OBJ)/abl/a_xs$*.o $(OBJ)/tcsc_mfma.o $(OBJ)/tcsc_small.o $(OBJ)/tcsc_format.o $(OBJ)/tcsc_cxx_abi.o $(OBJ)/bcsr_kernels.o $(OBJ)/bcsr_api.o -lpthread -L$(ROCM)/lib -lrocblas -Wl,-rpath,$(ROCM)/lib
+# Direct X staging (A/B, round 5, DESIGN.md §4 k_transpose): the variant and its target
+# lib/abl/libtcsc_amd_xs1.so are at commit b07f36f (measured slower, removed).
