@@ -219,8 +219,14 @@ def main():
     gather_s = timed(lambda: plan.sgemm_prepared(B, Y, cfg.M, ncols, variant, 0.2, sh), nsplit)
     kernel_s = gather_s
     combine = plan.combine_mode(cfg.M) if slices > 1 else None
-    kernel_name = "k_stream" + ((f" (+ in-launch {combine} combine)" if combine else " + k_reduce4") +
-                                f", {slices} K slices" if slices > 1 else "")
+    # the two halves per path: prepare_x / sgemm_prepared run k_transpose / k_stream
+    # on the gather path, k_split3 / k_gemm3 + k_fixup on the MFMA path
+    if path == "mfma":
+        kernel_name, stage_names = "k_gemm3 + k_fixup", ("k_split3", "k_gemm3 + k_fixup")
+    else:
+        kernel_name = "k_stream" + ((f" (+ in-launch {combine} combine)" if combine else " + k_reduce4") +
+                                    f", {slices} K slices" if slices > 1 else "")
+        stage_names = ("k_transpose", "gather")
 
     alt = None
     if distributed and args.scaling == "strong" and not args.no_alt_shard and args.shard_of <= 1:
@@ -299,7 +305,7 @@ def main():
                 # included): the HBM fraction that matches `value`
                 "step_achieved": algo_bytes / (elapsed_max / args.steps) / 1e9,
                 "step_frac": algo_bytes / (elapsed_max / args.steps) / 1e9 / HBM_PEAK_GBS,
-                "step_parts_ms": {"k_transpose": transpose_s * 1e3, "gather": gather_s * 1e3,
+                "step_parts_ms": {stage_names[0]: transpose_s * 1e3, stage_names[1]: gather_s * 1e3,
                                   "step_kernels": step_kernels_s * 1e3,
                                   "note": "HIP events on the launch stream, each averaged over the same launches"},
                 "lds_gather_frac": (cfg.M * nnz / kernel_s) / LDS_GATHER_PEAK,

@@ -348,22 +348,57 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
         __syncthreads();
     }
 
-    // epilogue: lane l holds rows 4*(l/16) + reg, column l % 16 of each block
+    // Epilogue: lane l holds rows 4*(l/16) + reg, column l % 16 of each 16 x 16
+    // block.  Stored as is, one instruction would write 4 rows x 16 columns of
+    // 4-B pieces (store-issue-bound); instead each pass of 64 tile rows is
+    // parked in the (now free) LDS, row stride TN + 4 floats (the 4 row groups
+    // of a block fall 16 banks apart), and read back as whole rows: 16-B
+    // stores, TN / 4 lanes per row.  Same values, same bits.
+    constexpr int PR = 64, SROW = TN + 4, LPR = TN / 4;  // rows per pass, staged row, lanes per row
+    static_assert(PR * SROW * 4 <= 2 * STAGE && TM % PR == 0 && 64 % LPR == 0, "epilogue staging");
+    // (the raw sums are parked; bias and PReLU are applied to the rows read
+    // back, where a lane's 4 columns stay the same: NW * 64 is a multiple of LPR)
+    static_assert((NW * 64) % LPR == 0, "a lane keeps its columns across the read-back");
+    float* stg = reinterpret_cast<float*>(lds);
+    const bool vec = (ldy & 3) == 0 && (reinterpret_cast<uintptr_t>(Y) & 15) == 0;
+    const int c4 = 4 * (threadIdx.x % LPR), col = n0 + c4;
+    f32x4 bq;
 #pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-        const int col = n0 + (wc * FJ + j) * 16 + (lane & 15);
-        const float b = col < N ? bias[col] : 0.0f;
+    for (int u = 0; u < 4; ++u) bq[u] = col + u < N ? bias[col + u] : 0.0f;
+#pragma unroll
+    for (int p = 0; p < TM / PR; ++p) {
 #pragma unroll
         for (int i = 0; i < FI; ++i) {
-            const int rowb = m0 + (wr * FI + i) * 16 + 4 * (lane >> 4);
+            if (((wr * FI + i) * 16) / PR != p) continue;  // uniform
+            const int rb = (wr * FI + i) * 16 - p * PR + 4 * (lane >> 4);
 #pragma unroll
-            for (int rg = 0; rg < 4; ++rg) {
-                const int row = rowb + rg;
-                float v = acc[i][j][rg] + b;
-                if (PRELU) v = (v < 0.0f) ? a * v : v;
-                if (row < M && col < N) __builtin_nontemporal_store(v, Y + (size_t)row * ldy + col);
+            for (int j = 0; j < FJ; ++j) {
+                const int c = (wc * FJ + j) * 16 + (lane & 15);
+#pragma unroll
+                for (int rg = 0; rg < 4; ++rg) stg[(rb + rg) * SROW + c] = acc[i][j][rg];
             }
         }
+        __syncthreads();
+        for (int e = threadIdx.x; e < PR * LPR; e += NW * 64) {
+            const int r = e / LPR;
+            const int row = m0 + p * PR + r;
+            if (row >= M) continue;
+            f32x4 v = *reinterpret_cast<const f32x4*>(stg + r * SROW + c4);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                v[u] = v[u] + bq[u];
+                if (PRELU) v[u] = (v[u] < 0.0f) ? a * v[u] : v[u];
+            }
+            float* dst = Y + (size_t)row * ldy + col;
+            if (vec && col + 3 < N) {
+                __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (col + u < N) __builtin_nontemporal_store(v[u], dst + u);
+            }
+        }
+        __syncthreads();  // the staging is reused by the next pass
     }
 }
 
