@@ -322,31 +322,75 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
 #pragma unroll
         for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // Half-step pipeline: the fragments of the two k halves live in two
+    // register sets, and the one barrier per k step sits between them.  Step t:
+    //   read kh 1 of t (set 1)  |  MFMAs on set 0 (kh 0 of t)
+    //   wait: set 1 read, DMA t+1 landed; barrier (every wave is done with t's
+    //   buffer, step t+1 is in LDS)
+    //   DMA t+2 into t's buffer, read kh 0 of t+1 (set 0)  |  MFMAs on set 1
+    // so each wave leaves the barrier with 32 MFMAs whose operands are already
+    // in registers, and the DMA issue and the next reads run under them.
+    bf16x8 af[2][FI], bfr[2][FJ];
+    auto frag = [&](int s, int buf, int kh) {
+        const char* sb = lds + buf * STAGE;
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+            bfr[s][j] = *reinterpret_cast<const bf16x8*>(sb + (PA + (wc * FJ + j) * 2) * 1024 + foff[kh]);
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+            af[s][i] = *reinterpret_cast<const bf16x8*>(sb + ((wr * FI + i) * 2) * 1024 + foff[kh]);
+    };
+    auto mma = [&](int s) {
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+            for (int j = 0; j < FJ; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][i], bfr[s][j], acc[i][j], 0, 0, 0);
+    };
+
+    // The order is pinned (the compiler otherwise hoists the barrier over the
+    // MFMAs and issues every read and DMA piece in one burst): each half step
+    // is one scheduling region, reads (and DMA pieces) one per MFMA pair.  The
+    // tail's DMA steps are clamped to the last step (a harmless reload into a
+    // buffer no one reads again) and its extra fragment read is discarded, so
+    // the body has no branch.
+    constexpr int NR = FI + FJ, NM = FI * FJ;
+    static_assert(2 * NR <= NM && PPW <= NR, "one read (and one DMA piece) per MFMA pair");
     dma(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    dma(min(1, ksteps - 1), 1);
+    frag(0, 0, 0);
     for (int t = 0; t < ksteps; ++t) {
         const int buf = t & 1;
-        if (t + 1 < ksteps) dma(t + 1, buf ^ 1);
-        const char* sb = lds + buf * STAGE;
+        frag(1, buf, 1);
+        mma(0);
 #pragma unroll
-        for (int kh = 0; kh < 2; ++kh) {
-            bf16x8 af[FI], bfr[FJ];
-#pragma unroll
-            for (int j = 0; j < FJ; ++j)
-                bfr[j] = *reinterpret_cast<const bf16x8*>(sb + (PA + (wc * FJ + j) * 2) * 1024 + foff[kh]);
-#pragma unroll
-            for (int i = 0; i < FI; ++i)
-                af[i] = *reinterpret_cast<const bf16x8*>(sb + ((wr * FI + i) * 2) * 1024 + foff[kh]);
-#pragma unroll
-            for (int i = 0; i < FI; ++i)
-#pragma unroll
-                for (int j = 0; j < FJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int k = 0; k < NR; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
         }
+        if constexpr (NM > 2 * NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
+        __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        __builtin_amdgcn_sched_barrier(0);
+        dma(min(t + 2, ksteps - 1), buf);
+        frag(0, buf ^ 1, 0);
+        mma(1);
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            if (k < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA piece)
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        }
+        if constexpr (NM > 2 * NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
+        __builtin_amdgcn_sched_barrier(0);
     }
+    // the tail's reload lands and every wave's last reads are done before the
+    // epilogue reuses the LDS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
 
     // Epilogue: lane l holds rows 4*(l/16) + reg, column l % 16 of each 16 x 16
     // block.  Stored as is, one instruction would write 4 rows x 16 columns of
