@@ -64,7 +64,7 @@ struct tcsc_gpu_plan {
     // three bf16 copies per column (cols x mfma_ldk(rows)), and the column
     // range's rebased CSC for the rows the bf16 split of X cannot carry.
     // Launches with M >= mfma_min_M take it; null when the plan is gather-only.
-    uint16_t* w3 = nullptr;
+    uint16_t* wt = nullptr;
     size_t mfma_bytes = 0;
     // the column range's rebased CSC (fast-order plans): the small-M path
     // walks it, the MFMA path's fixup recomputes flagged rows from it
@@ -232,7 +232,7 @@ int current_order() {
 // for smaller, less efficient GEMM shapes.
 constexpr double kMfmaDensity = 0.2;
 constexpr int kMfmaMinM = 64;
-constexpr double kMfmaMaxImageBytes = 16.0 * (1ull << 30);  // 3 bf16 copies of W
+constexpr double kMfmaMaxImageBytes = 16.0 * (1ull << 30);  // build: fp32 scratch + the bf16 W^T, 6 B a cell
 
 int path_mode() {  // 0 auto, 1 gather only, 2 mfma forced
     const char* e = std::getenv("TCSC_PATH");
@@ -253,7 +253,7 @@ size_t mfma_ws_bytes(int M, int K) { return align256((size_t)M * tcsc::mfma_ldk(
 bool valid_variant(int v) { return v >= TCSC_VARIANT_BASIC && v <= TCSC_VARIANT_SPARSE_GEMM; }
 bool is_prelu(int v) { return v >= TCSC_VARIANT_PRELU_BASIC && v <= TCSC_VARIANT_PRELU_ONTHEGO; }
 
-bool use_mfma(const tcsc_gpu_plan* p, int M) { return p->w3 && M >= p->mfma_min_M && p->rows > 0; }
+bool use_mfma(const tcsc_gpu_plan* p, int M) { return p->wt && M >= p->mfma_min_M && p->rows > 0; }
 
 rocblas_handle rocblas_for_device(int dev) {
     static std::mutex mu;
@@ -268,8 +268,8 @@ rocblas_handle rocblas_for_device(int dev) {
 }
 
 void free_mfma(tcsc_gpu_plan* p) {
-    if (p->w3) (void)hipFree(p->w3);
-    p->w3 = nullptr;
+    if (p->wt) (void)hipFree(p->wt);
+    p->wt = nullptr;
     p->mfma_bytes = 0;
 }
 
@@ -344,6 +344,8 @@ int maybe_build_mfma(tcsc_gpu_plan* p, const int* csp, const int* csn, const int
     const double cells = (double)p->rows * p->cols;
     const long long nnz = p->n_pos + p->n_neg;
     if (mode == 1 || cells == 0 || 6.0 * cells > kMfmaMaxImageBytes) return TCSC_OK;
+    // k_gemm3's DMA offsets are 32-bit bytes within a 256-row tile: K < ~2.8 M
+    if (512.0 * tcsc::mfma_ldk(p->rows) >= 4294967296.0) return TCSC_OK;
     if (mode == 0 && (nnz < kMfmaDensity * cells || p->rows < 64 || p->cols < 64)) return TCSC_OK;
     if (!p->crq) return TCSC_OK;  // the fixup needs the CSC copy
     const size_t n = (size_t)p->rows * p->cols;
@@ -352,16 +354,16 @@ int maybe_build_mfma(tcsc_gpu_plan* p, const int* csp, const int* csn, const int
         (void)hipGetLastError();
         return TCSC_OK;  // no room for the image: gather only
     }
-    const int ldk = tcsc::mfma_ldk(p->rows);
-    const size_t w3b = (size_t)p->cols * ldk * sizeof(uint16_t);
-    if (hipMalloc(&p->w3, w3b) != hipSuccess) {
+    const int ldw = tcsc::mfma_ldw(p->rows);
+    const size_t wtb = (size_t)p->cols * ldw * sizeof(uint16_t);
+    if (hipMalloc(&p->wt, wtb) != hipSuccess) {
         (void)hipGetLastError();
         free_mfma(p);
         return TCSC_OK;
     }
-    p->mfma_bytes = w3b;
+    p->mfma_bytes = wtb;
     HIP_TRY(hipMemsetAsync(bad.p, 0, sizeof(int), st));
-    HIP_TRY(tcsc::mfma_build_w3(csp, csn, rip, rin, col_begin, p->rows, p->cols, wf.as<float>(), p->w3, ldk,
+    HIP_TRY(tcsc::mfma_build_wt(csp, csn, rip, rin, col_begin, p->rows, p->cols, wf.as<float>(), p->wt, ldw,
                                 p->n_pos, p->n_neg, bad.as<int>(), st));
     int hbad = 0;
     HIP_TRY(hipMemcpyAsync(&hbad, bad.p, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -541,7 +543,7 @@ class DeviceGuard {
 
 namespace {
 // The MFMA path (stage 0: all; 1: split only; 2: GEMM + fixup on the staged
-// X3): k_split3 (X -> X3 + row flags), k_gemm3 (Y = act(X3 . W3T^T + B),
+// X3): k_split3 (X -> X3 + row flags), k_gemm3 (Y = act(X3 . WT^T + B),
 // the bias and PReLU in its store), k_fixup (the flagged rows, exact).
 int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy, int variant,
                float a, void* stream, float* ws, size_t ws_bytes, int stage) {
@@ -557,7 +559,7 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
     if (stage != 2) HIP_TRY(tcsc::mfma_split_x(dX, M, K, x3, ldk, flags, st));
     if (stage == 1) return TCSC_OK;
     const bool prelu = is_prelu(variant);
-    HIP_TRY(tcsc::mfma_gemm3(x3, p->w3, ldk, M, N, dB, dY, ldy, prelu, a, st));
+    HIP_TRY(tcsc::mfma_gemm3(x3, ldk, p->wt, tcsc::mfma_ldw(K), K, M, N, dB, dY, ldy, prelu, a, st));
     // fast order: bias after the sum for every variant
     HIP_TRY(tcsc::mfma_fixup(x3, M, K, ldk, p->ccq, p->crq, N, dB, dY, ldy, false, prelu, a, flags, st));
     return TCSC_OK;
@@ -815,7 +817,7 @@ int tcsc_gpu_plan_get_info(const tcsc_gpu_plan* p, tcsc_gpu_plan_info* info) {
     info->device_bytes = p->bytes + p->ws_bytes + p->mfma_bytes + p->csc_bytes + (p->chain_pos ? p->chain_pos->bytes : 0) +
                          (p->chain_neg ? p->chain_neg->bytes : 0);
     info->order = p->order;
-    info->mfma_min_M = p->w3 ? p->mfma_min_M : 0;
+    info->mfma_min_M = p->wt ? p->mfma_min_M : 0;
     return TCSC_OK;
 }
 
@@ -847,7 +849,7 @@ int tcsc_gpu_plan_reserve(tcsc_gpu_plan* p, int max_M) {
     }
     // both paths' needs at max_M: a later launch with fewer rows may take the other one
     size_t want = wanted_workspace(p, max_M);
-    if (p->w3) {
+    if (p->wt) {
         const int s = tcsc::choose_slices(max_M, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
                                           slices_override());
         want = std::max(want, tcsc::xt_bytes(max_M, p->rows) + tcsc::workspace_bytes(max_M, p->cols, s));

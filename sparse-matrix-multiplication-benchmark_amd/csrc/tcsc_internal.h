@@ -287,25 +287,27 @@ __host__ __device__ inline size_t csc_entry(const int* cq, int j, int i) {
 }
 
 // ---- MFMA path for near-dense W (tcsc_mfma.hip) ------------
-// X3 / W3T rows are ldk = mfma_ldk(K) bf16 long, in blocks of kMfmaBlk = 32
-// k (one MFMA's depth): [h | m | l] of block 0, of block 1, ... (X3) or
-// [w | w | w] per block (W3T), zeros past K and up to a multiple of the
-// GEMM's 64-deep k step.  Each MFMA thus adds one part of one block, and the
-// accumulation runs k-major (h, m, l of a block, then the next block): its
-// fp32 rounding error is about half that of a part-major [h | m | l] image
-// (the accumulator is not carried across K three times).
-constexpr int kMfmaBlk = 32;
+// X3 rows are ldk = mfma_ldk(K) bf16 long, in blocks of kMfmaBlk = 64 k (one
+// GEMM k step): [h | m | l] of block 0, of block 1, ..., zeros past K.  Each
+// part of a block is 128 B, one cache line, so the GEMM stages it in whole
+// lines.  W is stored once (WT, ncols x ldw = mfma_ldw(K)): the GEMM stages a
+// block of W once and multiplies it with the block's three parts in turn.
+// The accumulation runs k-major (h, m, l of a block, then the next block):
+// its fp32 rounding error is about half that of a part-major [h | m | l]
+// image (the accumulator is not carried across K three times).
+constexpr int kMfmaBlk = 64;
 __host__ __device__ inline int mfma_nblk(int K) { return (K + kMfmaBlk - 1) / kMfmaBlk; }
-__host__ __device__ inline int mfma_ldk(int K) { return (3 * kMfmaBlk * mfma_nblk(K) + 63) / 64 * 64; }
+__host__ __device__ inline int mfma_ldk(int K) { return 3 * kMfmaBlk * mfma_nblk(K); }
+__host__ __device__ inline int mfma_ldw(int K) { return kMfmaBlk * mfma_nblk(K); }
 __host__ __device__ inline int x3_index(int k, int part) {
     return (k / kMfmaBlk) * (3 * kMfmaBlk) + part * kMfmaBlk + k % kMfmaBlk;
 }
 // Build: wf (ncols x rows fp32 scratch) <- the +1/-1 entries of columns
-// [col_begin, col_begin+ncols) (absolute offsets), transposed; w3 <- W^T
-// with three bf16 copies per row (ncols x ldk).  *bad = 1 if a weight is
-// not exact in bf16.
-hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int rows,
-                         int ncols, float* wf, uint16_t* w3, int ldk, long long n_pos, long long n_neg, int* bad,
+// [col_begin, col_begin+ncols) (absolute offsets), transposed; wt <- W^T in
+// bf16 (ncols x ldw, zeros past rows).  *bad = 1 if a weight is not exact in
+// bf16.
+hipError_t mfma_build_wt(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int rows,
+                         int ncols, float* wf, uint16_t* wt, int ldw, long long n_pos, long long n_neg, int* bad,
                          hipStream_t st);
 // ---- small-M path (tcsc_small.hip) ----------------------------
 // X is staged in LDS as M row pairs [X | -0.0 | 0.. | -X | 0..] of 2*Kp
@@ -322,9 +324,10 @@ hipError_t launch_small_m(const float* X, int M, int K, const int* cq, const int
 // X (M x K) -> x3 (M x ldk bf16, [h | m | l | 0..]); flags[m] = 1 for the
 // rows the fixup recomputes, 0 otherwise (every row, every call).
 hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int* flags, hipStream_t st);
-// k_gemm3: Y = act(x3 . w3^T + B) on the matrix cores (bias after the sum).
-hipError_t mfma_gemm3(const uint16_t* x3, const uint16_t* w3, int ldk, int M, int N, const float* B, float* Y,
-                      int ldy, bool prelu, float a, hipStream_t st);
+// k_gemm3: Y = act(sum over blocks and parts of x3 . wt^T + B) on the matrix
+// cores (bias after the sum); K gives the block count.
+hipError_t mfma_gemm3(const uint16_t* x3, int ldk, const uint16_t* wt, int ldw, int K, int M, int N, const float* B,
+                      float* Y, int ldy, bool prelu, float a, hipStream_t st);
 // Rewrites the flagged rows in k_stream's fast order (no-op when none is).
 hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cq, const int* crq, int ncols,
                       const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a, const int* flags,

@@ -9,13 +9,13 @@
 // or small integers for duplicate rows), so each product is exact and the
 // GEMM
 //     Y = [h | m | l] . [W ; W ; W]           (M x 3K) . (3K x N)
-// (both operands stored k-contiguous, rows padded with zeros to a multiple of
-// the 64-deep k step: X3 is M x ldk, W3T is N x ldk) accumulates in fp32 on
-// the matrix cores -- k_gemm3, written here for gfx950: 256 x 256 tiles of 8
-// waves (v_mfma_f32_16x16x32_bf16), the k steps staged into a 2-deep LDS
-// ring by LDS-DMA with a conflict-free swizzle, bias (+ PReLU) fused into
-// the store.  Only the summation order differs from the gather's: the result
-// is within the fast-order bound, and bit-exact on integer-valued inputs.
+// accumulates in fp32 on the matrix cores -- k_gemm3, written here for
+// gfx950: 256 x 256 tiles of 8 waves (v_mfma_f32_16x16x32_bf16), X3 (M x ldk,
+// [h | m | l] per 64-k block) and W^T (N x ldw, stored once) staged into LDS
+// rings by LDS-DMA with a conflict-free swizzle, each W block multiplied with
+// the three parts of its X3 block in turn, bias (+ PReLU) fused into the
+// store.  Only the summation order differs from the gather's: the result is
+// within the fast-order bound, and bit-exact on integer-valued inputs.
 //
 // Rows the split cannot carry are recomputed by the gather order: a
 // non-finite x would make inf*0 = NaN in columns whose W is 0 there (the
@@ -89,7 +89,7 @@ __global__ void __launch_bounds__(256) k_split3(const float* __restrict__ X, int
         }
         uint16_t h[4], m[4], l[4];
         for (int j = 0; j < 4; ++j) fix |= split3(v[j], h[j], m[j], l[j]);
-        if (vec) {  // k0 .. k0+3 lie in one 32-k block
+        if (vec) {  // k0 .. k0+3 lie in one block
             typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
             *reinterpret_cast<u16x4*>(dst + x3_index(k0, 0)) = u16x4{h[0], h[1], h[2], h[3]};
             *reinterpret_cast<u16x4*>(dst + x3_index(k0, 1)) = u16x4{m[0], m[1], m[2], m[3]};
@@ -123,22 +123,18 @@ __global__ void k_w_scatter(const int* __restrict__ cs, const int* __restrict__ 
     for (int e = e0 + lane; e < e1; e += 64) atomicAdd(&WfT[(size_t)j * K + r[e]], sign);
 }
 
-// WfT (ncols x K fp32) -> W3T (ncols x ldk bf16): row n = [w | w | w | 0..],
-// so both GEMM operands run along k (the pad was zeroed before).  Values must
-// be integers of magnitude <= 256 to be exact in bf16; *bad = 1 otherwise.
-__global__ void k_w3_from(const float* __restrict__ WfT, int ncols, int K, uint16_t* __restrict__ W3T, int ldk,
+// WfT (ncols x K fp32) -> WT (ncols x ldw bf16, the pad zeroed before), k
+// contiguous like X3.  Values must be integers of magnitude <= 256 to be
+// exact in bf16; *bad = 1 otherwise.
+__global__ void k_wt_from(const float* __restrict__ WfT, int ncols, int K, uint16_t* __restrict__ WT, int ldw,
                           int* __restrict__ bad) {
     const long long n = (long long)ncols * K;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
          i += (long long)gridDim.x * blockDim.x) {
         const float w = WfT[i];
         if (fabsf(w) > 256.0f) *bad = 1;
-        const uint16_t b = (uint16_t)(f2u(w) >> 16);
         const long long j = i / K, k = i - j * K;
-        uint16_t* row = W3T + j * ldk;
-        row[x3_index((int)k, 0)] = b;
-        row[x3_index((int)k, 1)] = b;
-        row[x3_index((int)k, 2)] = b;
+        WT[j * ldw + k] = (uint16_t)(f2u(w) >> 16);
     }
 }
 
@@ -237,18 +233,21 @@ __global__ void __launch_bounds__(256) k_fixup(const uint16_t* __restrict__ X3, 
 
 // ---------------------------------------------------------------------------
 // k_gemm3: Y[m, n] = act(sum_k A[m, k] * Bt[n, k] + bias[n]), bf16 in, fp32
-// accumulate, A = X3 (M x ldk), Bt = W3T (N x ldk), ldk % 64 == 0.
+// accumulate, A = X3 (M x ldk: [h | m | l] per 64-k block), Bt = WT (N x ldw:
+// W's block once).
 //
 // * Tile TM x TN = (WM*FI*16) x (WN*FJ*16) per workgroup of WM*WN waves; a
 //   wave owns FI x FJ blocks of 16 x 16 (v_mfma_f32_16x16x32_bf16, 4 fp32
 //   accumulators per lane per block).  256 x 256 with 8 waves (2 x 4, 128 x
 //   64 per wave) for the large shapes; 128 x 128 with 4 waves for grids that
 //   would leave CUs idle.
-// * k steps of 64 staged in a 2-deep LDS ring by LDS-DMA
-//   (global_load_lds_dwordx4: 1 KiB per wave-instruction, no VGPRs): step
-//   t+1 is in flight while step t is multiplied; one vmcnt(0) + barrier per
-//   step.
-// * LDS image of a stage: A's rows, then B's, in 1-KiB pieces of 8 rows x 64
+// * The k loop runs over sub-steps (block, part): one part of X3's 64-k
+//   block against W's block.  A is staged per sub-step in a 2-slot ring, W
+//   once per block in a 2-slot ring of its own, by LDS-DMA
+//   (global_load_lds_dwordx4: 1 KiB per wave-instruction, no VGPRs).  The
+//   GEMM is bound by that staging (L2 -> LDS, ~43 GB/s per CU): staging W once
+//   per block instead of with every part moves 1/3 fewer bytes per MFMA.
+// * LDS image of a slot: 1-KiB pieces of 8 rows x 64
 //   k (128 B per row).  Inside a piece the 16-B granule g (8 k) of row r sits
 //   at slot 8r + (g ^ r): the DMA writes the piece lane-linear (lane = slot)
 //   from per-lane source addresses, and the MFMA fragment reads (lane l:
@@ -262,136 +261,27 @@ __global__ void __launch_bounds__(256) k_fixup(const uint16_t* __restrict__ X3, 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int WM, int WN, int FI, int FJ, bool PRELU>
-__global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
-                                                      int ldk, int M, int N, int ksteps,
-                                                      const float* __restrict__ bias, float* __restrict__ Y, int ldy,
-                                                      float a, int tiles_m, int tiles_n) {
-    constexpr int TM = WM * FI * 16, TN = WN * FJ * 16, NW = WM * WN;
-    constexpr int PA = TM / 8, PB = TN / 8;  // 1-KiB pieces per stage
-    constexpr int STAGE = (PA + PB) * 1024;
-    constexpr int PPW = (PA + PB) / NW;      // pieces each wave moves per stage
-    static_assert((PA + PB) % NW == 0, "whole pieces per wave");
-    __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];
-
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wr = wave / WN, wc = wave % WN;
-
-    // XCD-aware bijective renumbering, then groups of tiles_m x 4 tiles
+// XCD-aware bijective renumbering of blockIdx.x, then groups of tiles_m x 4
+// tiles: the workgroup's tile origin (m0, n0).
+template <int TM, int TN>
+__device__ __forceinline__ void gemm3_tile(int tiles_m, int tiles_n, int& m0, int& n0) {
     const int T = tiles_m * tiles_n, L = blockIdx.x;
     const int q = T >> 3, r = T & 7, x = L & 7;
     const int Lg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
     const int grp = Lg / (tiles_m * 4), idx = Lg % (tiles_m * 4);
     const int tm = idx % tiles_m, tn = grp * 4 + idx / tiles_m;
-    const int m0 = tm * TM, n0 = tn * TN;
+    m0 = tm * TM;
+    n0 = tn * TN;
+}
 
-    // this wave's DMA pieces: per-lane sources (row clamped into the matrix)
-    const int row_in = lane >> 3, gsel = (lane & 7) ^ row_in;
-    const uint16_t* src[PPW];
-    int dst[PPW];
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-        const int piece = wave * PPW + i;
-        if (piece < PA) {
-            const int rr = min(m0 + 8 * piece + row_in, M - 1);
-            src[i] = A + (size_t)rr * ldk + 8 * gsel;
-        } else {
-            const int rr = min(n0 + 8 * (piece - PA) + row_in, N - 1);
-            src[i] = Bt + (size_t)rr * ldk + 8 * gsel;
-        }
-        dst[i] = piece * 1024;
-    }
-    auto dma = [&](int kstep, int buf) {
-#pragma unroll
-        for (int i = 0; i < PPW; ++i)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[i] + (size_t)kstep * 64),
-                                             (__attribute__((address_space(3))) void*)(lds + buf * STAGE + dst[i]),
-                                             16, 0, 0);
-    };
-
-    // fragment read offsets inside a 16-row block (the swizzle above)
-    int foff[2];
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-        foff[kh] = ((lane & 15) >> 3) * 1024 + 16 * (8 * (lane & 7) + ((4 * kh + (lane >> 4)) ^ (lane & 7)));
-
-    f32x4 acc[FI][FJ];
-#pragma unroll
-    for (int i = 0; i < FI; ++i)
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // Half-step pipeline: the fragments of the two k halves live in two
-    // register sets, and the one barrier per k step sits between them.  Step t:
-    //   read kh 1 of t (set 1)  |  MFMAs on set 0 (kh 0 of t)
-    //   wait: set 1 read, DMA t+1 landed; barrier (every wave is done with t's
-    //   buffer, step t+1 is in LDS)
-    //   DMA t+2 into t's buffer, read kh 0 of t+1 (set 0)  |  MFMAs on set 1
-    // so each wave leaves the barrier with 32 MFMAs whose operands are already
-    // in registers, and the DMA issue and the next reads run under them.
-    bf16x8 af[2][FI], bfr[2][FJ];
-    auto frag = [&](int s, int buf, int kh) {
-        const char* sb = lds + buf * STAGE;
-#pragma unroll
-        for (int j = 0; j < FJ; ++j)
-            bfr[s][j] = *reinterpret_cast<const bf16x8*>(sb + (PA + (wc * FJ + j) * 2) * 1024 + foff[kh]);
-#pragma unroll
-        for (int i = 0; i < FI; ++i)
-            af[s][i] = *reinterpret_cast<const bf16x8*>(sb + ((wr * FI + i) * 2) * 1024 + foff[kh]);
-    };
-    auto mma = [&](int s) {
-#pragma unroll
-        for (int i = 0; i < FI; ++i)
-#pragma unroll
-            for (int j = 0; j < FJ; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][i], bfr[s][j], acc[i][j], 0, 0, 0);
-    };
-
-    // The order is pinned (the compiler otherwise hoists the barrier over the
-    // MFMAs and issues every read and DMA piece in one burst): each half step
-    // is one scheduling region, reads (and DMA pieces) one per MFMA pair.  The
-    // tail's DMA steps are clamped to the last step (a harmless reload into a
-    // buffer no one reads again) and its extra fragment read is discarded, so
-    // the body has no branch.
-    constexpr int NR = FI + FJ, NM = FI * FJ;
-    static_assert(2 * NR <= NM && PPW <= NR, "one read (and one DMA piece) per MFMA pair");
-    dma(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    dma(min(1, ksteps - 1), 1);
-    frag(0, 0, 0);
-    for (int t = 0; t < ksteps; ++t) {
-        const int buf = t & 1;
-        frag(1, buf, 1);
-        mma(0);
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
-        }
-        if constexpr (NM > 2 * NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        __builtin_amdgcn_sched_barrier(0);
-        dma(min(t + 2, ksteps - 1), buf);
-        frag(0, buf ^ 1, 0);
-        mma(1);
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            if (k < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA piece)
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        }
-        if constexpr (NM > 2 * NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    // the tail's reload lands and every wave's last reads are done before the
-    // epilogue reuses the LDS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
+// The k_gemm3 epilogue (both staging forms): Y = act(acc + bias) for the
+// workgroup's tile, the raw sums parked in the LDS (LDSB bytes, free once the
+// k loop has drained) and stored as whole rows.
+template <int WM, int WN, int FI, int FJ, bool PRELU, int LDSB>
+__device__ __forceinline__ void gemm3_store(const f32x4 (&acc)[FI][FJ], char* lds, int lane, int wr, int wc, int m0,
+                                            int n0, int M, int N, const float* __restrict__ bias,
+                                            float* __restrict__ Y, int ldy, float a) {
+    constexpr int TM = WM * FI * 16, TN = WN * FJ * 16, NW = WM * WN;
     // Epilogue: lane l holds rows 4*(l/16) + reg, column l % 16 of each 16 x 16
     // block.  Stored as is, one instruction would write 4 rows x 16 columns of
     // 4-B pieces (store-issue-bound); instead each pass of 64 tile rows is
@@ -399,7 +289,7 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
     // of a block fall 16 banks apart), and read back as whole rows: 16-B
     // stores, TN / 4 lanes per row.  Same values, same bits.
     constexpr int PR = 64, SROW = TN + 4, LPR = TN / 4;  // rows per pass, staged row, lanes per row
-    static_assert(PR * SROW * 4 <= 2 * STAGE && TM % PR == 0 && 64 % LPR == 0, "epilogue staging");
+    static_assert(PR * SROW * 4 <= LDSB && TM % PR == 0 && 64 % LPR == 0, "epilogue staging");
     // (the raw sums are parked; bias and PReLU are applied to the rows read
     // back, where a lane's 4 columns stay the same: NW * 64 is a multiple of LPR)
     static_assert((NW * 64) % LPR == 0, "a lane keeps its columns across the read-back");
@@ -446,6 +336,152 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
     }
 }
 
+template <int WM, int WN, int FI, int FJ, bool PRELU>
+__global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                                                      int ldk, int ldw, int M, int N, int nblk,
+                                                      const float* __restrict__ bias, float* __restrict__ Y, int ldy,
+                                                      float a, int tiles_m, int tiles_n) {
+    constexpr int TM = WM * FI * 16, TN = WN * FJ * 16, NW = WM * WN;
+    constexpr int PA = TM / 8, PB = TN / 8;  // 1-KiB pieces of a slot
+    constexpr int ASLOT = PA * 1024, BSLOT = PB * 1024, BOFF = 2 * ASLOT;
+    constexpr int PAW = PA / NW, PBW = PB / NW;  // pieces each wave moves per A / B slot
+    static_assert(PA % NW == 0 && PB % NW == 0, "whole pieces per wave");
+    __shared__ __attribute__((aligned(1024))) char lds[2 * ASLOT + 2 * BSLOT];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wave / WN, wc = wave % WN;
+
+    int m0, n0;
+    gemm3_tile<TM, TN>(tiles_m, tiles_n, m0, n0);
+
+    // this wave's DMA pieces: a uniform base (the operand's tile) plus per-lane
+    // byte offsets (rows clamped into the matrix; 32-bit: the saddr form)
+    const int row_in = lane >> 3, gsel = (lane & 7) ^ row_in;
+    uint32_t offa[PAW], offb[PBW];
+#pragma unroll
+    for (int i = 0; i < PAW; ++i)
+        offa[i] = 2u * (uint32_t)(min(8 * (wave * PAW + i) + row_in, M - 1 - m0) * ldk + 8 * gsel);
+#pragma unroll
+    for (int i = 0; i < PBW; ++i)
+        offb[i] = 2u * (uint32_t)(min(8 * (wave * PBW + i) + row_in, N - 1 - n0) * ldw + 8 * gsel);
+    const char* abase = reinterpret_cast<const char*>(A + (size_t)m0 * ldk);
+    const char* bbase = reinterpret_cast<const char*>(Bt + (size_t)n0 * ldw);
+    auto dma_a = [&](int blk, int part, int slot) {  // X3's part `part` of 64-k block `blk`
+        const char* g = abase + 2 * (size_t)(kMfmaBlk * (3 * blk + part));
+#pragma unroll
+        for (int i = 0; i < PAW; ++i)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g + offa[i]),
+                                             (__attribute__((address_space(3))) void*)(lds + slot * ASLOT +
+                                                                                       (wave * PAW + i) * 1024),
+                                             16, 0, 0);
+    };
+    auto dma_b = [&](int blk, int slot) {  // W's 64-k block `blk`
+        const char* g = bbase + 2 * (size_t)(kMfmaBlk * blk);
+#pragma unroll
+        for (int i = 0; i < PBW; ++i)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g + offb[i]),
+                                             (__attribute__((address_space(3))) void*)(lds + BOFF + slot * BSLOT +
+                                                                                       (wave * PBW + i) * 1024),
+                                             16, 0, 0);
+    };
+
+    // fragment read offsets inside a 16-row block (the swizzle above)
+    int foff[2];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+        foff[kh] = ((lane & 15) >> 3) * 1024 + 16 * (8 * (lane & 7) + ((4 * kh + (lane >> 4)) ^ (lane & 7)));
+
+    f32x4 acc[FI][FJ];
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // Half-step pipeline: the fragments of the two k halves live in two
+    // register sets, and the one barrier per sub-step sits between them.
+    // Sub-step s (block s / 3, part s % 3; A slot s & 1, B slot block & 1):
+    //   read kh 1 of s (set 1)  |  MFMAs on set 0 (kh 0 of s)
+    //   wait: set 1 read, DMA of s+1 landed; barrier (every wave is done with
+    //   s's A slot -- and, at a block's first part, with the previous block's
+    //   B slot -- and s+1 is in LDS)
+    //   DMA A of s+2 into s's slot (+ the next block's B at a first part),
+    //   read kh 0 of s+1 (set 0)  |  MFMAs on set 1
+    // so each wave leaves the barrier with 32 MFMAs whose operands are already
+    // in registers, and the DMA issue and the next reads run under them.
+    bf16x8 af[2][FI], bfr[2][FJ];
+    auto frag = [&](int set, int aslot, int bslot, int kh) {
+        const char* sa = lds + aslot * ASLOT;
+        const char* sb = lds + BOFF + bslot * BSLOT;
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+            bfr[set][j] = *reinterpret_cast<const bf16x8*>(sb + ((wc * FJ + j) * 2) * 1024 + foff[kh]);
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+            af[set][i] = *reinterpret_cast<const bf16x8*>(sa + ((wr * FI + i) * 2) * 1024 + foff[kh]);
+    };
+    auto mma = [&](int set) {
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+            for (int j = 0; j < FJ; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[set][i], bfr[set][j], acc[i][j], 0, 0, 0);
+    };
+
+    // The order is pinned (the compiler otherwise hoists the barrier over the
+    // MFMAs and issues every read and DMA piece in one burst): each half step
+    // is one scheduling region, one read per MFMA pair.  The tail's DMA is
+    // clamped to the last block (a harmless reload into a slot no one reads
+    // again) and its extra fragment read is discarded.
+    constexpr int NR = FI + FJ, NM = FI * FJ;
+    static_assert(2 * NR <= NM, "one read per MFMA pair");
+    auto pin = [&]() {
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
+        }
+        if constexpr (NM > 2 * NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    const int last = nblk - 1;
+    dma_a(0, 0, 0);
+    dma_b(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    dma_a(0, 1, 1);
+    frag(0, 0, 0, 0);
+    for (int blk = 0; blk < nblk; ++blk) {
+        const int bs = blk & 1;
+#pragma unroll
+        for (int part = 0; part < 3; ++part) {
+            const int as = (blk + part) & 1;  // (3 * blk + part) & 1
+            frag(1, as, bs, 1);
+            mma(0);
+            pin();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            __builtin_amdgcn_sched_barrier(0);
+            // A of sub-step s + 2: (blk, 2) after part 0, else (blk + 1, part - 1)
+            if (part == 0) {
+                dma_a(blk, 2, as);
+                dma_b(min(blk + 1, last), bs ^ 1);
+            } else {
+                const bool tail = blk == last;  // uniform: a scalar select, no branch
+                dma_a(tail ? last : blk + 1, tail ? 2 : part - 1, as);
+            }
+            frag(0, as ^ 1, part < 2 ? bs : bs ^ 1, 0);
+            mma(1);
+            pin();
+        }
+    }
+    // the tail's reloads land and every wave's last reads are done before the
+    // epilogue reuses the LDS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    gemm3_store<WM, WN, FI, FJ, PRELU, 2 * ASLOT + 2 * BSLOT>(acc, lds, lane, wr, wc, m0, n0, M, N, bias, Y, ldy, a);
+}
 
 }  // namespace
 
@@ -476,13 +512,13 @@ hipError_t csc_fill(const int* cp, const int* cn, const int* crp, const int* crn
     return hipGetLastError();
 }
 
-hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int rows,
-                         int ncols, float* wf, uint16_t* w3, int ldk, long long n_pos, long long n_neg, int* bad,
+hipError_t mfma_build_wt(const int* csp, const int* csn, const int* rip, const int* rin, int col_begin, int rows,
+                         int ncols, float* wf, uint16_t* wt, int ldw, long long n_pos, long long n_neg, int* bad,
                          hipStream_t st) {
     const long long n = (long long)rows * ncols;
     hipError_t e = hipMemsetAsync(wf, 0, (size_t)n * sizeof(float), st);
     if (e != hipSuccess) return e;
-    if ((e = hipMemsetAsync(w3, 0, (size_t)ncols * ldk * sizeof(uint16_t), st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(wt, 0, (size_t)ncols * ldw * sizeof(uint16_t), st)) != hipSuccess) return e;
     const int wpb = 4;  // waves (columns) per block
     if (n_pos > 0)
         hipLaunchKernelGGL(k_w_scatter, dim3((ncols + wpb - 1) / wpb), dim3(64 * wpb), 0, st, csp, rip, col_begin,
@@ -490,7 +526,7 @@ hipError_t mfma_build_w3(const int* csp, const int* csn, const int* rip, const i
     if (n_neg > 0)
         hipLaunchKernelGGL(k_w_scatter, dim3((ncols + wpb - 1) / wpb), dim3(64 * wpb), 0, st, csn, rin, col_begin,
                            ncols, rows, -1.0f, wf);
-    hipLaunchKernelGGL(k_w3_from, dim3(grid_of(n, 256)), dim3(256), 0, st, wf, ncols, rows, w3, ldk, bad);
+    hipLaunchKernelGGL(k_wt_from, dim3(grid_of(n, 256)), dim3(256), 0, st, wf, ncols, rows, wt, ldw, bad);
     return hipGetLastError();
 }
 
@@ -503,28 +539,28 @@ hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int
 // Tile choice: 256 x 256 (8 waves) unless that grid would leave more than
 // half of the 256 CUs idle, then 128 x 128 (4 waves).
 template <bool PRELU>
-static hipError_t launch_gemm3_t(const uint16_t* x3, const uint16_t* w3, int ldk, int M, int N, const float* B,
-                                 float* Y, int ldy, float a, hipStream_t st) {
-    const int ksteps = ldk / 64;
+static hipError_t launch_gemm3_t(const uint16_t* x3, int ldk, const uint16_t* wt, int ldw, int nblk, int M, int N,
+                                 const float* B, float* Y, int ldy, float a, hipStream_t st) {
     const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
     if (big >= 128) {
         const int tm = (M + 255) / 256, tn = (N + 255) / 256;
-        hipLaunchKernelGGL((k_gemm3<2, 4, 8, 4, PRELU>), dim3(tm * tn), dim3(512), 0, st, x3, w3, ldk, M, N, ksteps,
+        hipLaunchKernelGGL((k_gemm3<2, 4, 8, 4, PRELU>), dim3(tm * tn), dim3(512), 0, st, x3, wt, ldk, ldw, M, N, nblk,
                            B, Y, ldy, a, tm, tn);
     } else {
         const int tm = (M + 127) / 128, tn = (N + 127) / 128;
-        hipLaunchKernelGGL((k_gemm3<2, 2, 4, 4, PRELU>), dim3(tm * tn), dim3(256), 0, st, x3, w3, ldk, M, N, ksteps,
+        hipLaunchKernelGGL((k_gemm3<2, 2, 4, 4, PRELU>), dim3(tm * tn), dim3(256), 0, st, x3, wt, ldk, ldw, M, N, nblk,
                            B, Y, ldy, a, tm, tn);
     }
     return hipGetLastError();
 }
 
-hipError_t mfma_gemm3(const uint16_t* x3, const uint16_t* w3, int ldk, int M, int N, const float* B, float* Y,
-                      int ldy, bool prelu, float a, hipStream_t st) {
+hipError_t mfma_gemm3(const uint16_t* x3, int ldk, const uint16_t* wt, int ldw, int K, int M, int N, const float* B,
+                      float* Y, int ldy, bool prelu, float a, hipStream_t st) {
     if (M <= 0 || N <= 0) return hipSuccess;
-    if (ldk % 64 != 0) return hipErrorInvalidValue;
-    return prelu ? launch_gemm3_t<true>(x3, w3, ldk, M, N, B, Y, ldy, a, st)
-                 : launch_gemm3_t<false>(x3, w3, ldk, M, N, B, Y, ldy, a, st);
+    const int nblk = mfma_nblk(K);
+    if (nblk < 1 || ldk != mfma_ldk(K) || ldw != mfma_ldw(K)) return hipErrorInvalidValue;
+    return prelu ? launch_gemm3_t<true>(x3, ldk, wt, ldw, nblk, M, N, B, Y, ldy, a, st)
+                 : launch_gemm3_t<false>(x3, ldk, wt, ldw, nblk, M, N, B, Y, ldy, a, st);
 }
 
 hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cq, const int* crq, int ncols,
