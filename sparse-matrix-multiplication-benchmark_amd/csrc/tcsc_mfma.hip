@@ -28,6 +28,7 @@
 // k_stream's fast order (= the reference's dense.c gemm_basic order).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "tcsc_internal.h"
@@ -256,22 +257,24 @@ __global__ void __launch_bounds__(256) k_fixup(const uint16_t* __restrict__ X3, 
 //   cycles per read instead of 16-32 for a linear image).
 // * Rows past M / N load the last valid row (in bounds) and are not stored.
 // * Tile order: XCD-aware and bijective; an XCD's ~32 concurrent workgroups
-//   take 8 row tiles x 4 column tiles, sharing A and B tiles in its L2.
+//   take 4 row tiles x 8 column tiles, sharing A and W tiles in its L2.
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// XCD-aware bijective renumbering of blockIdx.x, then groups of tiles_m x 4
-// tiles: the workgroup's tile origin (m0, n0).
+// XCD-aware bijective renumbering of blockIdx.x (an XCD's workgroups get
+// consecutive numbers), then bands of gm row tiles walked column by column:
+// an XCD's ~32 concurrent workgroups take gm row tiles x 32 / gm column
+// tiles, sharing those A and W tiles in its L2.
 template <int TM, int TN>
-__device__ __forceinline__ void gemm3_tile(int tiles_m, int tiles_n, int& m0, int& n0) {
+__device__ __forceinline__ void gemm3_tile(int tiles_m, int tiles_n, int gm, int& m0, int& n0) {
     const int T = tiles_m * tiles_n, L = blockIdx.x;
     const int q = T >> 3, r = T & 7, x = L & 7;
     const int Lg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
-    const int grp = Lg / (tiles_m * 4), idx = Lg % (tiles_m * 4);
-    const int tm = idx % tiles_m, tn = grp * 4 + idx / tiles_m;
-    m0 = tm * TM;
-    n0 = tn * TN;
+    const int band = Lg / (gm * tiles_n), rb = Lg - band * gm * tiles_n;
+    const int g = min(gm, tiles_m - band * gm);  // the last band may be shorter
+    m0 = (band * gm + rb % g) * TM;
+    n0 = (rb / g) * TN;
 }
 
 // The k_gemm3 epilogue (both staging forms): Y = act(acc + bias) for the
@@ -340,7 +343,7 @@ template <int WM, int WN, int FI, int FJ, bool PRELU>
 __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                                                       int ldk, int ldw, int M, int N, int nblk,
                                                       const float* __restrict__ bias, float* __restrict__ Y, int ldy,
-                                                      float a, int tiles_m, int tiles_n) {
+                                                      float a, int tiles_m, int tiles_n, int gm) {
     constexpr int TM = WM * FI * 16, TN = WN * FJ * 16, NW = WM * WN;
     constexpr int PA = TM / 8, PB = TN / 8;  // 1-KiB pieces of a slot
     constexpr int ASLOT = PA * 1024, BSLOT = PB * 1024, BOFF = 2 * ASLOT;
@@ -353,7 +356,7 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
     const int wr = wave / WN, wc = wave % WN;
 
     int m0, n0;
-    gemm3_tile<TM, TN>(tiles_m, tiles_n, m0, n0);
+    gemm3_tile<TM, TN>(tiles_m, tiles_n, gm, m0, n0);
 
     // this wave's DMA pieces: a uniform base (the operand's tile) plus per-lane
     // byte offsets (rows clamped into the matrix; 32-bit: the saddr form)
@@ -542,14 +545,19 @@ template <bool PRELU>
 static hipError_t launch_gemm3_t(const uint16_t* x3, int ldk, const uint16_t* wt, int ldw, int nblk, int M, int N,
                                  const float* B, float* Y, int ldy, float a, hipStream_t st) {
     const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
+    // bands of 4 row tiles: an XCD's 32 workgroups share 4 A tiles (staged every
+    // sub-step) and 8 W tiles (once per block); 8 x 4 was 2 % slower at cfg 5
+    constexpr int kGm = 4;
     if (big >= 128) {
         const int tm = (M + 255) / 256, tn = (N + 255) / 256;
+        const int gm = std::min(kGm, tm);
         hipLaunchKernelGGL((k_gemm3<2, 4, 8, 4, PRELU>), dim3(tm * tn), dim3(512), 0, st, x3, wt, ldk, ldw, M, N, nblk,
-                           B, Y, ldy, a, tm, tn);
+                           B, Y, ldy, a, tm, tn, gm);
     } else {
         const int tm = (M + 127) / 128, tn = (N + 127) / 128;
+        const int gm = std::min(kGm, tm);
         hipLaunchKernelGGL((k_gemm3<2, 2, 4, 4, PRELU>), dim3(tm * tn), dim3(256), 0, st, x3, wt, ldk, ldw, M, N, nblk,
-                           B, Y, ldy, a, tm, tn);
+                           B, Y, ldy, a, tm, tn, gm);
     }
     return hipGetLastError();
 }
