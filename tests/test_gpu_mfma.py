@@ -105,6 +105,26 @@ def test_integer_inputs_bit_exact(gpu, oracle, path):
     W.free()
 
 
+@pytest.mark.parametrize("K", [40, 130, 333])
+def test_big_tiles_ragged_shapes_integer_exact(gpu, oracle, path, K):
+    """The 256 x 256 tiles (grids of >= 128 tiles): M = 2050 leaves a short last
+    band of row tiles in the XCD tile order and a ragged last tile, N = 4000 a
+    ragged last column tile; K = 40 is one 64-k block (the DMA tail clamps from
+    the first sub-step), 130 an odd block count, 333 a ragged last block.  The
+    path is forced: an automatic plan skips the image below 64 rows of W."""
+    path("mfma")
+    M, N = 2050, 4000
+    Wd = oracle.ternary((K, N), 0.5, 91 + K)
+    X, B = oracle.integers((M, K), 92 + K), oracle.integers((N,), 93 + K)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    Wref = oracle.tcsc_from_dense(Wd)
+    for variant in ("basic", "prelu_basic"):
+        Y, info = device_run(W, X, B, variant)
+        assert info["mfma_min_M"] == 1
+        np.testing.assert_array_equal(Y, oracle.sgemm(variant, X, Wref, B, 0.2), err_msg=variant)
+    W.free()
+
+
 def test_special_rows_match_the_gather_bit_for_bit(gpu, oracle, path, monkeypatch):
     monkeypatch.setenv("TCSC_SLICES", "1")  # the gather without split-K: one accumulator per output
     M, K, N = 96, 256, 200
