@@ -239,7 +239,7 @@ __global__ void __launch_bounds__(256) k_fixup(const uint16_t* __restrict__ X3, 
 //
 // * Tile TM x TN = (WM*FI*16) x (WN*FJ*16) per workgroup of WM*WN waves; a
 //   wave owns FI x FJ blocks of 16 x 16 (v_mfma_f32_16x16x32_bf16, 4 fp32
-//   accumulators per lane per block).  256 x 256 with 8 waves (2 x 4, 128 x
+//   accumulators per lane per block).  128 x 512 with 8 waves (1 x 8, 128 x
 //   64 per wave) for the large shapes; 128 x 128 with 4 waves for grids that
 //   would leave CUs idle.
 // * The k loop runs over sub-steps (block, part): one part of X3's 64-k
@@ -292,7 +292,7 @@ __device__ __forceinline__ void gemm3_store(const f32x4 (&acc)[FI][FJ], char* ld
     // of a block fall 16 banks apart), and read back as whole rows: 16-B
     // stores, TN / 4 lanes per row.  Same values, same bits.
     constexpr int PR = 64, SROW = TN + 4, LPR = TN / 4;  // rows per pass, staged row, lanes per row
-    static_assert(PR * SROW * 4 <= LDSB && TM % PR == 0 && 64 % LPR == 0, "epilogue staging");
+    static_assert(PR * SROW * 4 <= LDSB && TM % PR == 0 && (64 % LPR == 0 || LPR % 64 == 0), "epilogue staging");
     // (the raw sums are parked; bias and PReLU are applied to the rows read
     // back, where a lane's 4 columns stay the same: NW * 64 is a multiple of LPR)
     static_assert((NW * 64) % LPR == 0, "a lane keeps its columns across the read-back");
@@ -539,8 +539,8 @@ hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int
     return hipGetLastError();
 }
 
-// Tile choice: 256 x 256 (8 waves) unless that grid would leave more than
-// half of the 256 CUs idle, then 128 x 128 (4 waves).
+// Tile choice: 128 x 512 (8 waves) unless a grid of 256 x 256 tiles would
+// leave more than half of the 256 CUs idle, then 128 x 128 (4 waves).
 template <bool PRELU>
 static hipError_t launch_gemm3_t(const uint16_t* x3, int ldk, const uint16_t* wt, int ldw, int nblk, int M, int N,
                                  const float* B, float* Y, int ldy, float a, hipStream_t st) {
@@ -549,9 +549,12 @@ static hipError_t launch_gemm3_t(const uint16_t* x3, int ldk, const uint16_t* wt
     // sub-step) and 8 W tiles (once per block); 8 x 4 was 2 % slower at cfg 5
     constexpr int kGm = 4;
     if (big >= 128) {
-        const int tm = (M + 255) / 256, tn = (N + 255) / 256;
+        // 128 x 512 tiles of 8 waves (1 x 8, 128 x 64 each): A, staged every
+        // sub-step, is the narrow side (37.3 KiB staged per sub-step, 256 x 256
+        // tiles: 42.7; 1.4 % faster at cfg 5).  Its LDS is the whole 160 KiB.
+        const int tm = (M + 127) / 128, tn = (N + 511) / 512;
         const int gm = std::min(kGm, tm);
-        hipLaunchKernelGGL((k_gemm3<2, 4, 8, 4, PRELU>), dim3(tm * tn), dim3(512), 0, st, x3, wt, ldk, ldw, M, N, nblk,
+        hipLaunchKernelGGL((k_gemm3<1, 8, 8, 4, PRELU>), dim3(tm * tn), dim3(512), 0, st, x3, wt, ldk, ldw, M, N, nblk,
                            B, Y, ldy, a, tm, tn, gm);
     } else {
         const int tm = (M + 127) / 128, tn = (N + 127) / 128;

@@ -107,11 +107,12 @@ def test_integer_inputs_bit_exact(gpu, oracle, path):
 
 @pytest.mark.parametrize("K", [40, 130, 333])
 def test_big_tiles_ragged_shapes_integer_exact(gpu, oracle, path, K):
-    """The 256 x 256 tiles (grids of >= 128 tiles): M = 2050 leaves a short last
-    band of row tiles in the XCD tile order and a ragged last tile, N = 4000 a
-    ragged last column tile; K = 40 is one 64-k block (the DMA tail clamps from
-    the first sub-step), 130 an odd block count, 333 a ragged last block.  The
-    path is forced: an automatic plan skips the image below 64 rows of W."""
+    """The large tiles (128 x 512, for grids of >= 128 256 x 256 tiles): M = 2050
+    leaves a short last band of row tiles in the XCD tile order and a ragged
+    last tile, N = 4000 a ragged last column tile; K = 40 is one 64-k block
+    (the DMA tail clamps from the first sub-step), 130 an odd block count, 333
+    a ragged last block.  The path is forced: an automatic plan skips the
+    image below 64 rows of W."""
     path("mfma")
     M, N = 2050, 4000
     Wd = oracle.ternary((K, N), 0.5, 91 + K)
