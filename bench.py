@@ -512,9 +512,9 @@ def other_configs(args, tcsc_amd, workloads, dev, sh, timed, skip):
             "path": path,
         }
         if mfma:
-            # the split GEMM's depth: 3 parts of 32-k blocks, rounded up to the
-            # 64-deep k step (tcsc_internal.h mfma_ldk)
-            ldk = (3 * 32 * ((c.K + 31) // 32) + 63) // 64 * 64
+            # the split GEMM's depth: 3 parts of each 64-k block (tcsc_internal.h
+            # mfma_ldk = 3 * kMfmaBlk * ceil(K / kMfmaBlk), kMfmaBlk = 64)
+            ldk = 3 * 64 * ((c.K + 63) // 64)
             flops = 2.0 * c.M * c.N * ldk
             r["mfma_flops_per_step"] = flops
             r["mfma_frac"] = flops / t / MFMA_BF16_PEAK
