@@ -172,7 +172,9 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan *plan);
  * rows holding non-finite or tiny values (k_fixup) -- with the same accuracy
  * bounds as the gather.  It allocates nothing per launch and
  * keeps no state between launches, so graph replays with new X are exact.
- * $TCSC_PATH=gather|mfma at plan creation disables / forces the path.
+ * $TCSC_PATH=gather|mfma at plan creation disables / forces the path (the
+ * image is never built for K of ~2.8 M rows or more: k_gemm3's staging
+ * offsets are 32-bit; the gather serves those plans).
  * Thread safety: concurrent launches of ONE plan (on any streams) share its
  * workspace and are not supported; different plans are independent. */
 int tcsc_gpu_sgemm(const tcsc_gpu_plan *plan, const float *dX, const float *dB,
