@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <type_traits>
 
 #include "tcsc_internal.h"
 
@@ -361,13 +362,10 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
     // this wave's DMA pieces: a uniform base (the operand's tile) plus per-lane
     // byte offsets (rows clamped into the matrix; 32-bit: the saddr form)
     const int row_in = lane >> 3, gsel = (lane & 7) ^ row_in;
-    uint32_t offa[PAW], offb[PBW];
+    uint32_t offa[PAW];
 #pragma unroll
     for (int i = 0; i < PAW; ++i)
         offa[i] = 2u * (uint32_t)(min(8 * (wave * PAW + i) + row_in, M - 1 - m0) * ldk + 8 * gsel);
-#pragma unroll
-    for (int i = 0; i < PBW; ++i)
-        offb[i] = 2u * (uint32_t)(min(8 * (wave * PBW + i) + row_in, N - 1 - n0) * ldw + 8 * gsel);
     const char* abase = reinterpret_cast<const char*>(A + (size_t)m0 * ldk);
     const char* bbase = reinterpret_cast<const char*>(Bt + (size_t)n0 * ldw);
     auto dma_a = [&](int blk, int part, int slot) {  // X3's part `part` of 64-k block `blk`
@@ -379,11 +377,13 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
                                                                                        (wave * PAW + i) * 1024),
                                              16, 0, 0);
     };
-    auto dma_b = [&](int blk, int slot) {  // W's 64-k block `blk`
+    auto dma_b = [&](int blk, int slot) {  // W's 64-k block `blk` (offsets recomputed: once per block)
         const char* g = bbase + 2 * (size_t)(kMfmaBlk * blk);
 #pragma unroll
         for (int i = 0; i < PBW; ++i)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g + offb[i]),
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(
+                                                 g + 2u * (uint32_t)(min(8 * (wave * PBW + i) + row_in, N - 1 - n0) * ldw +
+                                                                     8 * gsel)),
                                              (__attribute__((address_space(3))) void*)(lds + BOFF + slot * BSLOT +
                                                                                        (wave * PBW + i) * 1024),
                                              16, 0, 0);
@@ -412,16 +412,21 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
     //   read kh 0 of s+1 (set 0)  |  MFMAs on set 1
     // so each wave leaves the barrier with 32 MFMAs whose operands are already
     // in registers, and the DMA issue and the next reads run under them.
+    // W's fragments are the same for a block's three parts: set kh of bfr is
+    // read at the block's first part and kept through its last (A's are read
+    // every sub-step).
     bf16x8 af[2][FI], bfr[2][FJ];
-    auto frag = [&](int set, int aslot, int bslot, int kh) {
+    auto frag_a = [&](int set, int aslot, int kh) {
         const char* sa = lds + aslot * ASLOT;
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+            af[set][i] = *reinterpret_cast<const bf16x8*>(sa + ((wr * FI + i) * 2) * 1024 + foff[kh]);
+    };
+    auto frag_b = [&](int set, int bslot, int kh) {
         const char* sb = lds + BOFF + bslot * BSLOT;
 #pragma unroll
         for (int j = 0; j < FJ; ++j)
             bfr[set][j] = *reinterpret_cast<const bf16x8*>(sb + ((wc * FJ + j) * 2) * 1024 + foff[kh]);
-#pragma unroll
-        for (int i = 0; i < FI; ++i)
-            af[set][i] = *reinterpret_cast<const bf16x8*>(sa + ((wr * FI + i) * 2) * 1024 + foff[kh]);
     };
     auto mma = [&](int set) {
 #pragma unroll
@@ -436,9 +441,10 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
     // is one scheduling region, one read per MFMA pair.  The tail's DMA is
     // clamped to the last block (a harmless reload into a slot no one reads
     // again) and its extra fragment read is discarded.
-    constexpr int NR = FI + FJ, NM = FI * FJ;
-    static_assert(2 * NR <= NM, "one read per MFMA pair");
-    auto pin = [&]() {
+    constexpr int NM = FI * FJ;
+    static_assert(2 * (FI + FJ) <= NM, "one read per MFMA pair");
+    auto pin = [&](auto nr_c) {  // nr reads, one per MFMA pair, then the rest of the MFMAs
+        constexpr int NR = decltype(nr_c)::value;
 #pragma unroll
         for (int k = 0; k < NR; ++k) {
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
@@ -447,21 +453,25 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
         if constexpr (NM > 2 * NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
         __builtin_amdgcn_sched_barrier(0);
     };
+    using with_b = std::integral_constant<int, FI + FJ>;
+    using a_only = std::integral_constant<int, FI>;
     const int last = nblk - 1;
     dma_a(0, 0, 0);
     dma_b(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     dma_a(0, 1, 1);
-    frag(0, 0, 0, 0);
+    frag_b(0, 0, 0);
+    frag_a(0, 0, 0);
     for (int blk = 0; blk < nblk; ++blk) {
         const int bs = blk & 1;
 #pragma unroll
         for (int part = 0; part < 3; ++part) {
             const int as = (blk + part) & 1;  // (3 * blk + part) & 1
-            frag(1, as, bs, 1);
+            if (part == 0) frag_b(1, bs, 1);
+            frag_a(1, as, 1);
             mma(0);
-            pin();
+            if (part == 0) pin(with_b{}); else pin(a_only{});
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             __builtin_amdgcn_sched_barrier(0);
@@ -473,9 +483,10 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
                 const bool tail = blk == last;  // uniform: a scalar select, no branch
                 dma_a(tail ? last : blk + 1, tail ? 2 : part - 1, as);
             }
-            frag(0, as ^ 1, part < 2 ? bs : bs ^ 1, 0);
+            if (part == 2) frag_b(0, bs ^ 1, 0);  // the next block's
+            frag_a(0, as ^ 1, 0);
             mma(1);
-            pin();
+            if (part == 2) pin(with_b{}); else pin(a_only{});
         }
     }
     // the tail's reloads land and every wave's last reads are done before the
