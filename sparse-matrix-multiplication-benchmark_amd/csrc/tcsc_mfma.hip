@@ -447,8 +447,8 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
         constexpr int NR = decltype(nr_c)::value;
 #pragma unroll
         for (int k = 0; k < NR; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA (first: its operands are the older reads)
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
         }
         if constexpr (NM > 2 * NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
         __builtin_amdgcn_sched_barrier(0);
