@@ -458,7 +458,9 @@ def host_api_line(tcsc_amd, cfg, ncols, variant, X, B, Y, csp, csn, rip, rin, ad
             "min_ms": min(ts) * 1e3, "first_call_ms": first * 1e3, "calls": calls,
             "pcie_bytes": 4 * (cfg.M * cfg.K + cfg.M * ncols + ncols),
             "bit_identical_to_device_api": same,
-            "note": "pageable host X/B/Y; H2D + kernels + D2H, row bands through pinned slots over 3 streams"}
+            "note": "pageable host X/B/Y; H2D + kernels + D2H, row bands through pinned slots over 3 streams; "
+                    "the host API's exact mode (K unsplit, no MFMA: dense.c gemm_basic's order), so its bits equal "
+                    "the device API's only where the device launch does not split K"}
 
 
 MFMA_BF16_PEAK = 2.5e15  # dense bf16 MFMA FLOP/s (MI355X_MICROARCH.md chip table, spec)

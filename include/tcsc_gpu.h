@@ -232,6 +232,21 @@ void tcsc_gpu_cache_clear(void);
 int tcsc_gpu_num_shards(void);
 void tcsc_gpu_set_num_shards(int shards);
 
+/* The host-pointer API (sparse/tcsc.h, include/sparse_gemm.h) runs in EXACT
+ * mode by default: every call sums each output in dense.c gemm_basic's order
+ * (y = 0; y += X*W over ascending k; y += B; then the PReLU for the PReLU
+ * variants) -- the fast order with K never split, never the MFMA path -- so
+ * its outputs equal the reference harness's own oracle bit for bit
+ * (main.cpp:307-366 checks tcsc_sgemm_basic / _optimized against it with an
+ * absolute 1e-4).  $TCSC_HOST_FAST=1 (read per call) lets host calls take the
+ * device API's fastest paths instead (MFMA, split K): within the fp32 bound
+ * of the exact sums, not bit-equal to gemm_basic. */
+
+/* Diagnostic build flags of the loaded library: 0 for the product build;
+ * bits 1 TCSC_ABLATION, 2 TCSC_NODMA, 4 TCSC_STAMPS, 8 TCSC_TRACE (timing-only
+ * builds of tools/ab.mk whose outputs are wrong by design). */
+int tcsc_gpu_build_flags(void);
+
 #ifdef __cplusplus
 }
 #endif

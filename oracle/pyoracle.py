@@ -465,3 +465,20 @@ def check_close(Y: np.ndarray, Y64: np.ndarray, S64: np.ndarray, prelu_a: float 
     err = np.abs(Y.astype(np.float64) - ref)
     ratio = float(np.max(err / bound)) if err.size else 0.0
     return bool(np.all(err <= bound)), ratio
+
+
+def assert_builder_matches(oracle: Oracle, dense: np.ndarray, csp, csn, rip, rin) -> None:
+    """Pin a device-built TCSC (the library's tcsc_gpu_from_dense) to the
+    oracle's tcsc_from_dense (tcsc.c:6-66, row-major restatement) of the same
+    dense matrix: all four arrays bit for bit.  Raises AssertionError naming
+    the first differing array and position."""
+    ref = oracle.tcsc_from_dense(dense, rowmajor=True)
+    got = [np.asarray(a, dtype=np.int32) for a in (csp, csn, rip, rin)]
+    for name, g, r in zip(("col_start_pos", "col_start_neg", "row_index_pos", "row_index_neg"), got, ref.arrays()):
+        if g.shape != r.shape:
+            raise AssertionError(f"device builder: {name} has {g.size} entries, the oracle {r.size}")
+        bad = np.flatnonzero(g != r)
+        if bad.size:
+            i = int(bad[0])
+            raise AssertionError(f"device builder: {name} differs at {bad.size} entries, first [{i}]: "
+                                 f"{int(g[i])} vs oracle {int(r[i])}")

@@ -280,12 +280,34 @@ void free_csc(tcsc_gpu_plan* p) {
     p->csc_bytes = 0;
 }
 
-// The rebased CSC copy of a fast-order plan's column range (4 bytes per
-// nonzero + 8 per column).  Not building it is not an error: the small-M
-// path and the MFMA path are then off for this plan.
+// Whether maybe_build_mfma would build the MFMA image for this plan (before
+// the allocation and bf16-exactness checks): the path mode, the image's size
+// and K limits and, by default, the density threshold.
+bool mfma_wanted(const tcsc_gpu_plan* p, bool allow_mfma) {
+    const int mode = path_mode();
+    const double cells = (double)p->rows * p->cols;
+    const long long nnz = p->n_pos + p->n_neg;
+    if (!allow_mfma || mode == 1 || cells == 0 || 6.0 * cells > kMfmaMaxImageBytes) return false;
+    // k_gemm3's DMA offsets are 32-bit bytes within a 256-row tile: K < ~2.8 M
+    if (512.0 * tcsc::mfma_ldk(p->rows) >= 4294967296.0) return false;
+    return !(mode == 0 && (nnz < kMfmaDensity * cells || p->rows < 64 || p->cols < 64));
+}
+
+// The merged CSC copy of a fast-order plan's column range (the quad layout of
+// tcsc_internal.h: one 4-byte entry per nonzero, each 64-column group padded
+// to its longest column, plus 4 bytes per group).  Only its two consumers
+// want it: the small-M path (K small enough for X to fit the LDS) and the
+// MFMA path's fixup.  A group padded far past its nonzeros (a few long
+// columns among short ones) is not worth its memory: above kCscMaxPad times
+// the nonzeros the copy is dropped.  Not building it is not an error: the
+// small-M path and the MFMA path are then off for this plan.
+constexpr double kCscMaxPad = 4.0;
 int build_csc(tcsc_gpu_plan* p, const int* csp, const int* csn, const int* rip, const int* rin, int col_begin,
-              hipStream_t st) {
-    if (p->cols == 0 || p->rows >= (1 << 28)) return TCSC_OK;  // entries are 4*row (< 2^30) with a sign bit
+              bool allow_mfma, hipStream_t st) {
+    // entries are byte offsets 4*k (+1 rows) and 4*Kp + 4*k (-1 rows), Kp = K + 1
+    // rounded up to 4: below 2^31 while K < 2^27 - 4
+    if (p->cols == 0 || p->rows >= (1 << 27) - 4) return TCSC_OK;
+    if (!tcsc::small_m_fits(1, p->rows) && !mfma_wanted(p, allow_mfma)) return TCSC_OK;
     const int nc = p->cols, ng = tcsc::csc_groups(nc);
     size_t tb = 0;
     DevBuf tcp, tcn, trp, trn, gq, tmp;  // scratch: the rebased per-sign lists, merged into crq
@@ -304,6 +326,11 @@ int build_csc(tcsc_gpu_plan* p, const int* csp, const int* csn, const int* rip, 
     HIP_TRY(hipMemcpyAsync(&quads, p->ccq + ng, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const size_t ent = tcsc::csc_quad_entries(quads);
+    const double nnz = (double)(p->n_pos + p->n_neg);
+    if ((double)ent > kCscMaxPad * nnz + (double)tcsc::csc_quad_entries(16LL * ng)) {
+        free_csc(p);  // padding-dominated: gather only
+        return TCSC_OK;
+    }
     if (hipMalloc(&p->crq, ent * sizeof(int)) != hipSuccess) {
         (void)hipGetLastError();
         free_csc(p);
@@ -339,14 +366,9 @@ bool use_small(const tcsc_gpu_plan* p, int M) {
 // Adds the MFMA image to a fast-order plan when the path mode and the density
 // call for it.  Not building it is never an error: the gather serves every M.
 int maybe_build_mfma(tcsc_gpu_plan* p, const int* csp, const int* csn, const int* rip, const int* rin, int col_begin,
-                     hipStream_t st) {
+                     bool allow_mfma, hipStream_t st) {
     const int mode = path_mode();
-    const double cells = (double)p->rows * p->cols;
-    const long long nnz = p->n_pos + p->n_neg;
-    if (mode == 1 || cells == 0 || 6.0 * cells > kMfmaMaxImageBytes) return TCSC_OK;
-    // k_gemm3's DMA offsets are 32-bit bytes within a 256-row tile: K < ~2.8 M
-    if (512.0 * tcsc::mfma_ldk(p->rows) >= 4294967296.0) return TCSC_OK;
-    if (mode == 0 && (nnz < kMfmaDensity * cells || p->rows < 64 || p->cols < 64)) return TCSC_OK;
+    if (!mfma_wanted(p, allow_mfma)) return TCSC_OK;
     if (!p->crq) return TCSC_OK;  // the fixup needs the CSC copy
     const size_t n = (size_t)p->rows * p->cols;
     DevBuf wf, bad;
@@ -375,14 +397,15 @@ int maybe_build_mfma(tcsc_gpu_plan* p, const int* csp, const int* csn, const int
 
 // The plan, plus -- in reference order -- its two one-sign chains: the same
 // build on the same arrays with the other sign's col_start replaced by zeros.
+// allow_mfma false: never the MFMA image (the host API's exact mode).
 int build_plan_ordered(int rows, int col_begin, int ncols, long long n_pos, long long n_neg, const int* csp,
                        const int* csn, const int* rip, const int* rin, int device, hipStream_t st, int order,
-                       tcsc_gpu_plan** out) {
+                       tcsc_gpu_plan** out, bool allow_mfma = true) {
     int rc = build_plan(rows, col_begin, ncols, n_pos, n_neg, csp, csn, rip, rin, device, st, out);
     if (rc != TCSC_OK) return rc;
     if (order != TCSC_ORDER_REFERENCE) {
-        rc = build_csc(*out, csp, csn, rip, rin, col_begin, st);
-        if (rc == TCSC_OK) rc = maybe_build_mfma(*out, csp, csn, rip, rin, col_begin, st);
+        rc = build_csc(*out, csp, csn, rip, rin, col_begin, allow_mfma, st);
+        if (rc == TCSC_OK) rc = maybe_build_mfma(*out, csp, csn, rip, rin, col_begin, allow_mfma, st);
         if (rc != TCSC_OK) {
             tcsc_gpu_plan_destroy(*out);
             *out = nullptr;
@@ -692,8 +715,9 @@ int tcsc_gpu_device_count(void) { return device_count_raw(); }
 
 const char* tcsc_gpu_last_error(void) { return g_last_error.c_str(); }
 
-int tcsc_gpu_plan_create(const tcsc_t* W, int col_begin, int col_end, int device, void* stream,
-                         tcsc_gpu_plan** out) {
+// tcsc_gpu_plan_create; allow_mfma false for the host API's exact mode
+static int plan_create_impl(const tcsc_t* W, int col_begin, int col_end, int device, void* stream, bool allow_mfma,
+                            tcsc_gpu_plan** out) {
     if (!W || !out || col_begin < 0 || col_end > W->cols || col_begin > col_end || W->rows < 0) {
         set_error("tcsc_gpu_plan_create: bad arguments");
         return TCSC_E_ARG;
@@ -735,9 +759,14 @@ int tcsc_gpu_plan_create(const tcsc_t* W, int col_begin, int col_end, int device
     if (q1 > q0)
         HIP_TRY(hipMemcpyAsync(drin.p, hrin, (size_t)(q1 - q0) * sizeof(int), hipMemcpyHostToDevice, st));
     rc = build_plan_ordered(W->rows, 0, nc, p1 - p0, q1 - q0, dcsp.as<int>(), dcsn.as<int>(), drip.as<int>(),
-                            drin.as<int>(), device, st, current_order(), out);
+                            drin.as<int>(), device, st, current_order(), out, allow_mfma);
     if (rc == TCSC_OK) (*out)->col_begin = col_begin;
     return rc;
+}
+
+int tcsc_gpu_plan_create(const tcsc_t* W, int col_begin, int col_end, int device, void* stream,
+                         tcsc_gpu_plan** out) {
+    return plan_create_impl(W, col_begin, col_end, device, stream, true, out);
 }
 
 int tcsc_gpu_plan_create_device(int rows, int cols, const int* d_csp, const int* d_csn, const int* d_rip,
@@ -1112,6 +1141,22 @@ int shard_axis() {
     return (e && std::strcmp(e, "rows") == 0) ? kAxisRows : kAxisCols;
 }
 
+// Host API exact mode (the default; TCSC_HOST_FAST=1 turns it off).  The
+// reference's harness validates tcsc_sgemm_basic / _optimized against its
+// dense oracle, dense.c:64-77 gemm_basic (y = 0; y += X*W over ascending k;
+// Y = y + B), with an absolute 1e-4 (main.cpp:307-333, dense.c:42-59), and
+// the three PReLU variants against each other (main.cpp:357-366).  So every
+// host call sums in exactly that order: the fast order with K never split
+// (the gather with one K-slice, or the small-M path), never the MFMA path,
+// whose bf16 x3 sums are rounded in its own blocked order.
+// The outputs are then gemm_basic's bits (+ PReLU) on every shape, shard count
+// and shard axis.  With TCSC_HOST_FAST=1 host calls take the device API's
+// fastest paths (MFMA at density >= 0.2, split K): within the fp32 bound.
+bool host_exact() {
+    const char* e = std::getenv("TCSC_HOST_FAST");
+    return !(e && std::atoi(e) != 0);
+}
+
 struct CacheEntry {
     // fingerprint: the shape, the array addresses and a hash of the array
     // contents (tcsc_fingerprint), checked on every call, so rebuilding the
@@ -1123,6 +1168,8 @@ struct CacheEntry {
     int order = TCSC_ORDER_FAST;  // the summation order the shards' plans were built for
     int axis = kAxisCols;         // shard_axis() when built
     int blocks = 1;               // S: row or column blocks per call
+    bool exact = true;            // host_exact() when built: no MFMA image, K never split
+    unsigned traced = 0;          // variants already reported under $TCSC_HOST_PATHS
     std::vector<Shard> shards;    // cols: one per column block; rows: one per device used
 };
 
@@ -1369,7 +1416,7 @@ bool fingerprint_matches(const CacheEntry& e, const tcsc_t* W, uint64_t content)
     return e.rows == W->rows && e.cols == W->cols && e.n_pos == W->n_elem_pos && e.n_neg == W->n_elem_neg &&
            e.csp == W->col_start_pos && e.csn == W->col_start_neg && e.rip == W->row_index_pos &&
            e.rin == W->row_index_neg && e.content == content && e.order == current_order() &&
-           e.axis == shard_axis();
+           e.axis == shard_axis() && e.exact == host_exact();
 }
 
 [[noreturn]] void die() {
@@ -1445,6 +1492,7 @@ int get_entry_locked(const tcsc_t* W, uint64_t content, CacheEntry** out) {
     e.content = content;
     e.order = current_order();
     e.axis = shard_axis();
+    e.exact = host_exact();
     int S = num_shards_locked(ndev);
     if (e.axis == kAxisCols && S > W->cols && W->cols > 0) S = W->cols;
     if (S < 1) S = 1;
@@ -1460,7 +1508,7 @@ int get_entry_locked(const tcsc_t* W, uint64_t content, CacheEntry** out) {
             DeviceGuard dg(sh.device);
             if (!ds.stream) HIP_TRY(hipStreamCreateWithFlags(&ds.stream, hipStreamNonBlocking));
         }
-        int rc = tcsc_gpu_plan_create(W, sh.c0, sh.c1, sh.device, ds.stream, &sh.plan);
+        int rc = plan_create_impl(W, sh.c0, sh.c1, sh.device, ds.stream, !e.exact, &sh.plan);
         if (rc != TCSC_OK) {
             destroy_entry(e);
             return rc;
@@ -1523,13 +1571,14 @@ int ensure_events(std::vector<hipEvent_t>& v, size_t n, unsigned flags = hipEven
 // whole job, so the bits equal one launch's.
 constexpr int kNoPinned = -1;  // run_bands: no pinned slots, take the unbanded path
 int run_bands(int dev, DevState& ds, const Shard& sh, int m0, int M, int nb, const float* X, const float* B, float* Y,
-              int N, int K, int variant, float a) {
+              int N, int K, int variant, float a, bool exact) {
     const tcsc_gpu_plan* p = sh.plan;
     const int nc = sh.c1 - sh.c0;
     hipStream_t st = ds.stream;
     int rc;
-    const int s = tcsc::choose_slices(M, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
-                                      slices_override());
+    const int s = exact ? 1
+                        : tcsc::choose_slices(M, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
+                                              slices_override());
     const int rows_per = (M + nb - 1) / nb;
     const int bm = (rows_per + tcsc::kTM - 1) / tcsc::kTM * tcsc::kTM;
     const int nbands = (M + bm - 1) / bm;
@@ -1667,7 +1716,7 @@ int run_bands(int dev, DevState& ds, const Shard& sh, int m0, int M, int nb, con
 // slice, the launch, D2H of the (m1-m0) x (c1-c0) block into Y.  A large job
 // runs as a pipeline of row bands over three streams (host_bands).
 int run_device(int dev, const std::vector<Job>& jobs, const float* X, const float* B, float* Y, int N, int K,
-               int variant, float a) {
+               int variant, float a, bool exact) {
     DeviceGuard dg(dev);
     DevState& ds = g_dev[dev];
     hipStream_t st = ds.stream;
@@ -1680,7 +1729,7 @@ int run_device(int dev, const std::vector<Job>& jobs, const float* X, const floa
         if ((rc = ensure(&ds.b, &ds.b_cap, (size_t)nc * sizeof(float))) != TCSC_OK) return rc;
         if ((rc = ensure(&ds.y, &ds.y_cap, (size_t)M * nc * sizeof(float))) != TCSC_OK) return rc;
         if (nb > 1) {
-            rc = run_bands(dev, ds, *j.sh, j.m0, M, nb, X, B, Y, N, K, variant, a);
+            rc = run_bands(dev, ds, *j.sh, j.m0, M, nb, X, B, Y, N, K, variant, a, exact);
             if (rc == TCSC_OK) {
                 staged0 = j.m0;
                 staged1 = j.m1;
@@ -1698,7 +1747,8 @@ int run_device(int dev, const std::vector<Job>& jobs, const float* X, const floa
         const size_t wsb = wanted_workspace(sh->plan, M);
         if (wsb && (rc = ensure(&ds.ws, &ds.ws_cap, wsb)) != TCSC_OK) return rc;
         HIP_TRY(hipMemcpyAsync(ds.b, B + sh->c0, (size_t)nc * sizeof(float), hipMemcpyHostToDevice, st));
-        if ((rc = sgemm_ws(sh->plan, ds.x, ds.b, ds.y, M, nc, variant, a, st, ds.ws, ds.ws_cap)) != TCSC_OK)
+        if ((rc = sgemm_ws(sh->plan, ds.x, ds.b, ds.y, M, nc, variant, a, st, ds.ws, ds.ws_cap, 0, exact ? 1 : 0)) !=
+            TCSC_OK)
             return rc;
         HIP_TRY(hipMemcpy2DAsync(Y + (size_t)j.m0 * N + sh->c0, (size_t)N * sizeof(float), ds.y,
                                  (size_t)nc * sizeof(float), (size_t)nc * sizeof(float), M, hipMemcpyDeviceToHost,
@@ -1707,6 +1757,33 @@ int run_device(int dev, const std::vector<Job>& jobs, const float* X, const floa
     }
     HIP_TRY(hipStreamSynchronize(st));
     return TCSC_OK;
+}
+
+// $TCSC_HOST_PATHS: one stderr line per matrix and variant (its first call),
+// naming the path and K-split each block took, so a failed validation in a
+// harness run (tests/test_reference_main_gpu.py) says which code computed it.
+void trace_paths(CacheEntry& e, int variant, int M, int N, int K) {
+    static const bool on = std::getenv("TCSC_HOST_PATHS") != nullptr;
+    if (!on || variant < 0 || variant >= 32 || (e.traced & (1u << variant))) return;
+    e.traced |= 1u << variant;
+    static const char* kNames[] = {"basic", "optimized", "prelu_basic", "prelu_separate", "prelu_onthego",
+                                   "sparse_gemm"};
+    std::string paths;
+    for (const Shard& sh : e.shards) {
+        const tcsc_gpu_plan* p = sh.plan;
+        const int rows = e.axis == kAxisRows ? (M + e.blocks - 1) / e.blocks : M;
+        const char* path = use_mfma(p, rows) ? "mfma" : use_small(p, rows) ? "small" : "gather";
+        int s = 1;
+        if (!e.exact && !use_mfma(p, rows) && !use_small(p, rows))
+            s = tcsc::choose_slices(rows, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
+                                    slices_override());
+        char buf[96];
+        std::snprintf(buf, sizeof buf, "%s%s/s%d", paths.empty() ? "" : ",", path, s);
+        paths += buf;
+    }
+    std::fprintf(stderr, "[tcsc_amd] path: %s M=%d N=%d K=%d blocks=%d axis=%s exact=%d -> %s\n",
+                 variant <= TCSC_VARIANT_SPARSE_GEMM ? kNames[variant] : "?", M, N, K, e.blocks,
+                 e.axis == kAxisRows ? "rows" : "cols", e.exact ? 1 : 0, paths.c_str());
 }
 
 void host_sgemm(int variant, const float* X, const tcsc_t* W, const float* B, float a, float* Y, int M, int N,
@@ -1755,13 +1832,13 @@ void host_sgemm(int variant, const float* X, const tcsc_t* W, const float* B, fl
         std::vector<int> used;
         for (size_t d = 0; d < per_dev.size(); ++d)
             if (!per_dev[d].empty()) used.push_back((int)d);
-        if (used.size() == 1) return run_device(used[0], per_dev[used[0]], X, B, Y, N, K, variant, a);
+        if (used.size() == 1) return run_device(used[0], per_dev[used[0]], X, B, Y, N, K, variant, a, ce->exact);
         std::vector<int> rcs(used.size(), TCSC_OK);
         std::vector<std::string> errs(used.size());
         std::vector<std::thread> th;
         for (size_t i = 0; i < used.size(); ++i)
             th.emplace_back([&, i] {
-                rcs[i] = run_device(used[i], per_dev[used[i]], X, B, Y, N, K, variant, a);
+                rcs[i] = run_device(used[i], per_dev[used[i]], X, B, Y, N, K, variant, a, ce->exact);
                 if (rcs[i] != TCSC_OK) errs[i] = g_last_error;  // thread-local
             });
         for (auto& t : th) t.join();
@@ -1787,6 +1864,7 @@ void host_sgemm(int variant, const float* X, const tcsc_t* W, const float* B, fl
     if (trace)
         std::fprintf(stderr, "[tcsc_amd] host call: %.1f us (%s%s)\n", us(),
                      speculative ? "cached plan, fingerprint overlapped" : "plan built", rerun ? ", rerun" : "");
+    if (rc == TCSC_OK) trace_paths(*e, variant, M, N, K);
     report(rc);
 }
 

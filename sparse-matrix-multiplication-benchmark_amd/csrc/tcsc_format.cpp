@@ -169,10 +169,13 @@ tcsc_t* tcsc_from_dense(dense_t dense, int rows, int cols) {
     bool gpu = n >= (1LL << 24);  // ~64 MB and up: PCIe + device beats two host passes
     if (mode && std::strcmp(mode, "host") == 0) gpu = false;
     if (mode && std::strcmp(mode, "gpu") == 0) gpu = true;
+    static const bool trace = std::getenv("TCSC_HOST_PATHS") != nullptr;
     if (gpu && tcsc_gpu_device_count() > 0) {
         tcsc_t* t = from_dense_gpu(dense, rows, cols);
+        if (trace) std::fprintf(stderr, "[tcsc_amd] tcsc_from_dense %dx%d: device builder%s\n", rows, cols, t ? "" : " failed");
         if (t || (mode && std::strcmp(mode, "gpu") == 0)) return t;
     }
+    if (trace) std::fprintf(stderr, "[tcsc_amd] tcsc_from_dense %dx%d: host builder\n", rows, cols);
     return from_dense_host(dense, rows, cols);
 }
 

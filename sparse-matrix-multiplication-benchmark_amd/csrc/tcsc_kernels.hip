@@ -565,7 +565,10 @@ __device__ __forceinline__ void combine_tile(float* ws, int M, int ncols, const 
     const int m0 = t.rt * kTM, c0 = t.cb * kWgCols;
     const size_t slab = (size_t)M * ncols;
     constexpr int nq = kWgCols / 4;
-    auto reduce_band = [&](int q, bool own) {  // own: slab q's band q is in this workgroup's LDS
+    // own: slab q's band q is in this workgroup's LDS; poison: a band whose
+    // owner never marked it (the bounded wait below ran out, i.e. a broken
+    // launch) is written as quiet NaN, never finalized from an unpublished slab
+    auto reduce_band = [&](int q, bool own, bool poison = false) {
         const int r0 = kTM * q / Z, r1 = kTM * (q + 1) / Z;
         for (int i = threadIdx.x; i < (r1 - r0) * nq; i += kWaves * 64) {
             const int row = m0 + r0 + i / nq, col = c0 + 4 * (i % nq);
@@ -604,6 +607,7 @@ __device__ __forceinline__ void combine_tile(float* ws, int M, int ncols, const 
                 v.z = (v.z < 0.0f) ? a * v.z : v.z;
                 v.w = (v.w < 0.0f) ? a * v.w : v.w;
             }
+            if (poison) v = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
             typedef float nt4 __attribute__((ext_vector_type(4)));
             nt4 o = {v.x, v.y, v.z, v.w};
             __builtin_nontemporal_store(o, reinterpret_cast<nt4*>(Y + (size_t)row * ldy + col));
@@ -645,7 +649,9 @@ __device__ __forceinline__ void combine_tile(float* ws, int M, int ncols, const 
                 flag[1] = (int)v;
             }
             __syncthreads();
-            if (__builtin_amdgcn_readfirstlane(flag[1]) == 2) reduce_band(q, false);
+            const int fq = __builtin_amdgcn_readfirstlane(flag[1]);
+            if (fq == 2) reduce_band(q, false);
+            else if (fq == 0) reduce_band(q, false, true);  // timed out: NaN, not a stale slab
         }
     }
     __syncthreads();
@@ -849,6 +855,7 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
     // bits.  The first finisher never waits, so no residency is assumed.
     const bool own_lds = OUT == 2 && gridDim.z == 4;  // combine_tile: the own band stays in the LDS
     int pair_role = 0;  // OUT 3: 0 = the tile's first slice to finish, 1 = the second
+    int pair_poison = 0;  // OUT 3: the partner's slab was never published (a bounded wait ran out): Y = NaN
     const bool pair_split = OUT == 3 && (combine_giveup & 2);  // OUT 3: split halves (resident grid)
     unsigned* const pw = OUT == 3 ? ccnt + (size_t)(t.rt * (int)gridDim.x + t.cb) * kCombineWords : nullptr;
     auto epilogue = [&](auto how_) {
@@ -863,18 +870,23 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                 int r = __hip_atomic_fetch_add(pw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u ? 0 : 1;
                 if (r == 1 && !pair_split) {
                     // the partner has arrived, so it is running and will publish: the bound
-                    // (100 ms) only keeps a broken launch from hanging the device
+                    // (100 ms) only keeps a broken launch from hanging the device, and
+                    // running out of it poisons the tile (NaN) instead of reading a stale slab
                     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                    while (__hip_atomic_load(pw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+                    bool ready;
+                    while (!(ready = __hip_atomic_load(pw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) &&
                            __builtin_amdgcn_s_memrealtime() - t0 < 10000000ull)
                         __builtin_amdgcn_s_sleep(2);
+                    if (!ready) r |= 2;
                     __hip_atomic_store(pw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(pw + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 role[0] = r;
             }
             __syncthreads();
-            pair_role = __builtin_amdgcn_readfirstlane(role[0]);
+            const int rv = __builtin_amdgcn_readfirstlane(role[0]);
+            pair_role = rv & 1;
+            pair_poison = rv >> 1;
         }
         constexpr int kQ = kCW / 4;                 // 16-B quads of a wave's row
         constexpr int kEpiRows = 64;                // tile rows per pass
@@ -981,6 +993,10 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                                     o.z = (o.z < 0.0f) ? a * o.z : o.z;
                                     o.w = (o.w < 0.0f) ? a * o.w : o.w;
                                 }
+                                if (pair_poison) {
+                                    const float qn = __builtin_nanf("");
+                                    o = make_float4(qn, qn, qn, qn);
+                                }
                                 typedef float nt4 __attribute__((ext_vector_type(4)));
                                 nt4 w = {o.x, o.y, o.z, o.w};
                                 __builtin_nontemporal_store(w, reinterpret_cast<nt4*>(Y + (size_t)row * ldy + col));
@@ -1060,16 +1076,21 @@ k_stream(const float* __restrict__ XT, int ldxt, int M, int K, const int2* __res
                         pw + 2, &expect, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     d = mine ? 0 : 1;  // 1: F gave up and stored rows 128..255 as well
                     // F has arrived, so it is running and publishes its half without
-                    // waiting; the bound (100 ms) only keeps a broken launch from hanging
+                    // waiting; the bound (100 ms) only keeps a broken launch from hanging,
+                    // and running out of it poisons what S finalizes (NaN)
                     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                    while (__hip_atomic_load(pw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+                    bool ready;
+                    while (!(ready = __hip_atomic_load(pw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) &&
                            __builtin_amdgcn_s_memrealtime() - t0 < 10000000ull)
                         __builtin_amdgcn_s_sleep(2);
+                    if (!ready) d |= 2;
                 }
                 dec[0] = d;
             }
             __syncthreads();
-            const int d = __builtin_amdgcn_readfirstlane(dec[0]);
+            const int dv = __builtin_amdgcn_readfirstlane(dec[0]);
+            const int d = dv & 1;
+            if (!first) pair_poison = dv >> 1;
             if (first) {
                 if (d == 0) {  // give the second half up: store it, then try to hand it over
                     pass(2, false);
@@ -1666,6 +1687,28 @@ hipError_t exclusive_scan_i32(const int* in, int* out, int n, void* tmp, size_t 
 }
 
 int ldxt_for(int M) { return ldxt_of(M); }
+
+}  // namespace tcsc
+
+// include/tcsc_gpu.h: which diagnostic macros this kernel object was built with
+extern "C" __attribute__((visibility("default"))) int tcsc_gpu_build_flags(void) {
+    int f = 0;
+#ifdef TCSC_ABLATION
+    f |= 1;
+#endif
+#ifdef TCSC_NODMA
+    f |= 2;
+#endif
+#ifdef TCSC_STAMPS
+    f |= 4;
+#endif
+#ifdef TCSC_TRACE
+    f |= 8;
+#endif
+    return f;
+}
+
+namespace tcsc {
 
 #ifdef TCSC_STAMPS
 extern "C" __attribute__((visibility("default"))) int tcsc_debug_stamps(void* dst, size_t bytes) {

@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_gpu_plan_reserve", "tcsc_gpu_plan_destroy", "tcsc_gpu_sgemm", "tcsc_gpu_prepare_x",
     "tcsc_gpu_sgemm_prepared", "tcsc_gpu_from_dense", "tcsc_gpu_dense_sgemm", "tcsc_gpu_last_error",
     "tcsc_gpu_cache_clear", "tcsc_gpu_num_shards", "tcsc_gpu_set_num_shards", "tcsc_gpu_set_order",
-    "tcsc_gpu_get_order", "tcsc_gpu_launch_info", "tcsc_gpu_launch_combine",
+    "tcsc_gpu_get_order", "tcsc_gpu_launch_info", "tcsc_gpu_launch_combine", "tcsc_gpu_build_flags",
     # include/sparse/bcsr.h
     "bcsr_from_dense", "bcsr_sgemm_basic", "bcsr_sgemm_prelu_basic", "bcsr_sgemm_avx", "bcsr_sgemm_prelu_avx",
     "bcsr_sgemm_avx2", "bcsr_free",
@@ -109,6 +109,13 @@ def lib():
     except ImportError:
         pass
     L = C.CDLL(LIB_PATH)
+    # the timing-only diagnostic builds of tools/ab.mk compute wrong results by
+    # design: never under a parity test or a bench line unless asked for
+    L.tcsc_gpu_build_flags.restype = C.c_int
+    flags = int(L.tcsc_gpu_build_flags())
+    if flags and os.environ.get("TCSC_ALLOW_DIAG") != "1":
+        raise TcscError(f"{LIB_PATH} is a diagnostic build (flags {flags:#x}: ablation/no-DMA/stamps/trace, "
+                        "results wrong by design); set TCSC_ALLOW_DIAG=1 to load it anyway")
     vp, i, f = C.c_void_p, C.c_int, C.c_float
     P = C.POINTER(tcsc_t)
     L.tcsc_from_dense.argtypes = [_f32p, i, i]

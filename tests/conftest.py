@@ -22,16 +22,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: full BASELINE-size cases")
     config.addinivalue_line("markers", "config_parity: the BASELINE-config / golden-fixture parity checks; "
                                        "collected first so that a -x stop elsewhere never hides a config")
+    config.addinivalue_line("markers", "run_last: long end-to-end runs (the reference's own harness), collected "
+                                       "after everything else so a -x stop there hides no parity test")
 
 
 def pytest_collection_modifyitems(session, config, items):
-    """Run every `config_parity` test before everything else (stable order
-    inside both groups): the driver runs `pytest -x`, and the per-config
-    parity verdict must not depend on an unrelated test further down."""
+    """Run every `config_parity` test before everything else and every
+    `run_last` test after everything else (stable order inside each group):
+    the driver runs `pytest -x`, and the per-row parity verdict must not
+    depend on an unrelated test, or on a long end-to-end run, further up."""
     first = [it for it in items if it.get_closest_marker("config_parity")]
-    if first:
-        rest = [it for it in items if not it.get_closest_marker("config_parity")]
-        items[:] = first + rest
+    last = [it for it in items if it.get_closest_marker("run_last") and not it.get_closest_marker("config_parity")]
+    rest = [it for it in items if not it.get_closest_marker("config_parity") and not it.get_closest_marker("run_last")]
+    items[:] = first + rest + last
 
 
 def load_golden(name):

@@ -53,6 +53,7 @@ def variants_of(g):
     return [v for v in pyoracle.BCSR_VARIANTS if "Y_" + v in g]
 
 
+@pytest.mark.config_parity
 @pytest.mark.parametrize("name", BCSR_GOLDEN_NAMES)
 def test_host_api_all_variants(gpu, name):
     g = load_bcsr_golden(name)
@@ -63,6 +64,7 @@ def test_host_api_all_variants(gpu, name):
     W.free()
 
 
+@pytest.mark.config_parity
 @pytest.mark.parametrize("name", ["empty_block_rows_4x8", "m9_k40_n42_2x3", "nonternary_2x8"])
 def test_host_api_on_reference_arrays(gpu, name):
     """The reference's own bcsr_from_dense arrays (not ours) through the
@@ -132,7 +134,11 @@ def test_bcsr_1x8_equals_tcsc_basic(gpu, torch_cuda, oracle, monkeypatch):
     (TCSC_SLICES=1; this grid is small enough for the cost model to split
     it), except where the bias goes: the TCSC fast order adds it after the
     sum (dense.c's gemm_basic order).  With a zero bias the
-    two orders are the same arithmetic: bit-identical outputs."""
+    two orders are the same arithmetic: bit-identical outputs.  The bias
+    path is cross-checked too: a nonzero integer bias on integer
+    X makes every order exact, so bias-first BCSR and bias-last TCSC must
+    agree bit for bit, for basic and prelu_basic; a nonzero float bias on
+    float X keeps both within the fp32 bound of the exact sums."""
     monkeypatch.setenv("TCSC_SLICES", "1")
     torch = torch_cuda
     dev = torch.device("cuda:0")
@@ -152,6 +158,23 @@ def test_bcsr_1x8_equals_tcsc_basic(gpu, torch_cuda, oracle, monkeypatch):
     pt.sgemm(dX, dB, Yt, M, N, "basic", 0.0, st)
     torch.cuda.synchronize()
     assert torch.equal(Yb, Yt)
+    Xi, Bi = oracle.integers((M, K), 83), oracle.integers((N,), 84, 64)
+    assert np.any(Bi != 0)
+    dXi, dBi = torch.from_numpy(Xi).to(dev), torch.from_numpy(Bi).to(dev)
+    for variant, a in (("basic", 0.0), ("prelu_basic", 0.25)):
+        pb.sgemm(dXi, dBi, Yb, M, N, K, N, variant, a, st)
+        pt.sgemm(dXi, dBi, Yt, M, N, variant, a, st)
+        torch.cuda.synchronize()
+        assert torch.equal(Yb, Yt), variant
+    Bf = oracle.uniform((N,), 85)
+    dBf = torch.from_numpy(Bf).to(dev)
+    pb.sgemm(dX, dBf, Yb, M, N, K, N, "basic", 0.0, st)
+    pt.sgemm(dX, dBf, Yt, M, N, "basic", 0.0, st)
+    torch.cuda.synchronize()
+    Y64, S64 = oracle.f64_rows(X, oracle.tcsc_from_dense(Wd), Bf)
+    for Y in (Yb, Yt):
+        ok, ratio = pyoracle.check_close(Y.cpu().numpy(), Y64, S64)
+        assert ok, ratio
     pb.destroy()
     pt.destroy()
 

@@ -30,7 +30,11 @@ def gpu():
 
 @pytest.fixture
 def path(monkeypatch):
-    """path(mode): TCSC_PATH for plans created from now on (host-API cache dropped)."""
+    """path(mode): TCSC_PATH for plans created from now on (host-API cache
+    dropped).  The host API runs in its fast mode here (TCSC_HOST_FAST=1), so
+    its calls take the MFMA path as the device API's do; its default exact
+    mode never does (tests/test_host_exact.py)."""
+    monkeypatch.setenv("TCSC_HOST_FAST", "1")
 
     def set_mode(mode):
         if mode is None:
@@ -41,6 +45,7 @@ def path(monkeypatch):
 
     yield set_mode
     monkeypatch.delenv("TCSC_PATH", raising=False)
+    monkeypatch.delenv("TCSC_HOST_FAST", raising=False)
     tcsc_amd.cache_clear()
 
 

@@ -74,6 +74,7 @@ def test_host_api_all_variants(gpu, oracle, name):
     W.free()
 
 
+@pytest.mark.config_parity
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
 def test_gpu_tcsc_from_dense_bitexact(gpu, name, monkeypatch):
     monkeypatch.setenv("TCSC_BUILDER", "gpu")
@@ -84,7 +85,9 @@ def test_gpu_tcsc_from_dense_bitexact(gpu, name, monkeypatch):
     W.free()
 
 
-def test_device_api_matches_host_api(gpu, torch_cuda, oracle):
+def test_device_api_matches_host_api(gpu, torch_cuda, oracle, monkeypatch):
+    """The device API with K unsplit equals the host API's exact mode."""
+    monkeypatch.setenv("TCSC_SLICES", "1")
     torch = torch_cuda
     g = load_golden("cfg1")
     W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
@@ -106,6 +109,7 @@ def test_device_api_matches_host_api(gpu, torch_cuda, oracle):
     plan.destroy()
 
 
+@pytest.mark.config_parity
 @pytest.mark.parametrize("name", ["cfg1", "cfg1_int", "edge_k_not_mult4", "edge_ragged_n65", "edge_m1"])
 def test_dense_baseline_matches_reference(gpu, torch_cuda, oracle, name):
     """the dense GPU baseline (rocBLAS fp32 + bias/PReLU
@@ -161,17 +165,18 @@ def test_prepare_then_gather_equals_sgemm(gpu, torch_cuda, name):
 
 @pytest.mark.parametrize("axis", ["rows", "cols"])
 @pytest.mark.parametrize("shards", [2, 3, 5])
-def test_multi_shard_host_path_equals_single(gpu, shards, axis, monkeypatch):
+def test_multi_shard_host_path_equals_single(gpu, oracle, shards, axis, monkeypatch):
     """The host API's blocks (one per GPU on a node; several per device here)
     concatenate to the single-block result bit for bit: column blocks
-    (TCSC_SHARD_AXIS=cols, the default) and row blocks.  Row blocks of a few
-    rows take the small-M path, whose sums are in the fast order; the whole
-    launch is held to the same order (the gather, K unsplit) so that the
-    comparison is bit for bit whatever path a block's M selects."""
+    (TCSC_SHARD_AXIS=cols, the default) and row blocks, with the default
+    environment.  Row blocks of a few rows take the small-M path and the
+    single block the gather; the host API's exact mode keeps K
+    unsplit on both, so both sum in gemm_basic's order and the bits cannot
+    depend on the shard count or axis.  Both equal the dense
+    oracle's gemm_basic + PReLU bit for bit."""
+    for k in ("TCSC_PATH", "TCSC_SLICES", "TCSC_HOST_FAST"):
+        monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("TCSC_SHARD_AXIS", axis)
-    if axis == "rows":
-        monkeypatch.setenv("TCSC_PATH", "gather")
-        monkeypatch.setenv("TCSC_SLICES", "1")
     g = load_golden("grid_m16_k512_n1024_nz8")
     W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
     tcsc_amd.set_num_shards(1)
@@ -181,7 +186,9 @@ def test_multi_shard_host_path_equals_single(gpu, shards, axis, monkeypatch):
         Ys = tcsc_amd.sgemm("prelu_onthego", g["X"], W, g["B"], 0.2)
     finally:
         tcsc_amd.set_num_shards(0)
-    np.testing.assert_array_equal(Ys, Y1)
+    np.testing.assert_array_equal(Ys.view(np.uint32), Y1.view(np.uint32))
+    want = pyoracle.prelu(oracle.gemm_basic(g["X"], g["Wd"].astype(np.float32), g["B"]), 0.2)
+    np.testing.assert_array_equal(Y1.view(np.uint32), want.view(np.uint32))
     W.free()
 
 
@@ -209,11 +216,18 @@ def test_multi_shard_host_path_large(gpu, oracle, axis, monkeypatch):
     W.free()
 
 
+@pytest.mark.parametrize("host_fast", ["0", "1"])
 @pytest.mark.parametrize("M,K,N,bands", [(1024, 1500, 700, 4), (1100, 700, 300, 3), (2000, 2600, 96, 8)])
-def test_host_bands_bit_identical(gpu, torch_cuda, oracle, M, K, N, bands, monkeypatch):
+def test_host_bands_bit_identical(gpu, torch_cuda, oracle, M, K, N, bands, host_fast, monkeypatch):
     """The host API's copy/compute pipeline (row bands over three streams,
-    TCSC_HOST_BANDS) gives the bits of one device launch, split-K included
-    (N=96: few column blocks, so K is split), ragged last band included."""
+    TCSC_HOST_BANDS) gives the bits of one device launch, ragged last band
+    included: in the host API's exact mode (host_fast 0) the device launch
+    with K unsplit, in its fast mode the device launch with the cost model's
+    split-K (N=96: few column blocks, so K is split)."""
+    monkeypatch.setenv("TCSC_HOST_FAST", host_fast)
+    if host_fast == "0":
+        monkeypatch.setenv("TCSC_SLICES", "1")
+    tcsc_amd.cache_clear()
     torch = torch_cuda
     Wd = oracle.ternary((K, N), 0.05, 700 + M)
     W = tcsc_amd.TcscMatrix.from_dense(Wd)
@@ -298,7 +312,11 @@ def test_zero_sized_calls(gpu, torch_cuda):
 # ---------------------------------------------------------------------------
 # Full BASELINE sizes (device API, sampled-row exact checks + properties)
 # ---------------------------------------------------------------------------
-def run_device_cfg(torch, cfg, variant, x=None):
+def run_device_cfg(torch, cfg, variant, oracle, x=None):
+    """BASELINE config cfg on the device API with W built on the GPU; the
+    built arrays are pinned to the oracle's tcsc_from_dense of the same dense
+    W first (all four arrays, bit for bit), so a builder error cannot hide
+    behind a parity check that feeds the builder's own arrays to the oracle."""
     dev = torch.device("cuda:0")
     inp = workloads.make_device_inputs(cfg, 0, cfg.N, dev)
     if x is not None:
@@ -310,7 +328,9 @@ def run_device_cfg(torch, cfg, variant, x=None):
     rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
     rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
     tcsc_amd.gpu_from_dense(inp["Wd"], K, N, csp, csn, rip, rin)
-    del inp["Wd"]
+    torch.cuda.synchronize()
+    pyoracle.assert_builder_matches(oracle, inp.pop("Wd").cpu().numpy(), csp.cpu().numpy(), csn.cpu().numpy(),
+                                    rip[:npos].cpu().numpy(), rin[:nneg].cpu().numpy())
     plan = tcsc_amd.Plan.from_device(K, N, csp, csn, rip, rin)
     plan.reserve(cfg.M)
     Y = torch.empty((cfg.M, N), device=dev)
@@ -326,7 +346,7 @@ def run_device_cfg(torch, cfg, variant, x=None):
 def test_baseline_config_sampled_rows(gpu, torch_cuda, oracle, cfg_idx):
     torch = torch_cuda
     cfg = workloads.CONFIGS[cfg_idx]
-    inp, W, Y, plan = run_device_cfg(torch, cfg, cfg.variant)
+    inp, W, Y, plan = run_device_cfg(torch, cfg, cfg.variant, oracle)
     rows = np.unique(np.concatenate([[0, 1, cfg.M - 1], np.random.default_rng(cfg_idx).integers(0, cfg.M, 29)]))
     Xs = inp["X"][torch.from_numpy(rows).to(inp["X"].device)].cpu().numpy()
     B = inp["B"].cpu().numpy()
@@ -443,6 +463,7 @@ def test_host_bands_with_blocks_bit_identical(gpu, oracle, axis, shards, bands, 
     W.free()
 
 
+@pytest.mark.config_parity
 @pytest.mark.parametrize("rows,cols", [(1, 1), (7, 300), (257, 513), (1000, 64), (17_000_000, 3)])
 def test_gpu_from_dense_tiles_bitexact(gpu, torch_cuda, oracle, rows, cols):
     """The tiled device builder (row tiles of 256, taller past 65535 tiles)
@@ -526,6 +547,9 @@ def test_cfg4_eight_way_shards_full_size(gpu, torch_cuda, oracle, axis):
     rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
     rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
     tcsc_amd.gpu_from_dense(inp["Wd"], K, N, csp, csn, rip, rin)
+    torch.cuda.synchronize()
+    pyoracle.assert_builder_matches(oracle, inp["Wd"].cpu().numpy(), csp.cpu().numpy(), csn.cpu().numpy(),
+                                    rip[:npos].cpu().numpy(), rin[:nneg].cpu().numpy())
     X, B = inp["X"], inp["B"]
     # |b| + sum_{P u Q} |x| per element (the bound's scale): the dense product on magnitudes
     S = torch.empty((M, N), device=dev)

@@ -101,7 +101,9 @@ def test_baseline_sizes_sampled_rows_bit_exact(reference_order, oracle, cfg_idx)
     rip = torch.empty(max(npos, 1), dtype=torch.int32, device=dev)
     rin = torch.empty(max(nneg, 1), dtype=torch.int32, device=dev)
     tcsc_amd.gpu_from_dense(inp["Wd"], K, N, csp, csn, rip, rin)
-    del inp["Wd"]
+    torch.cuda.synchronize()
+    pyoracle.assert_builder_matches(oracle, inp.pop("Wd").cpu().numpy(), csp.cpu().numpy(), csn.cpu().numpy(),
+                                    rip[:npos].cpu().numpy(), rin[:nneg].cpu().numpy())
     plan = tcsc_amd.Plan.from_device(K, N, csp, csn, rip, rin)
     plan.reserve(cfg.M)
     W = pyoracle.TCSC(K, N, csp.cpu().numpy(), csn.cpu().numpy(), rip[:npos].cpu().numpy(),

@@ -105,6 +105,7 @@ def _run(args, tmp_path, timeout=300):
 
 
 @pytest.mark.gpu
+@pytest.mark.config_parity
 def test_driver_baseline_config_device(tmp_path):
     out, recs = _run(["--config", "2", "--warmup", "2", "--reps", "5"], tmp_path)
     assert [r["algorithm"] for r in recs] == list(ALGOS)
@@ -143,6 +144,7 @@ def _library_nnz(seed, M, K, N, nz):
 
 
 @pytest.mark.gpu
+@pytest.mark.config_parity
 def test_driver_reference_cases_host_api(tmp_path):
     """main.cpp's five cases through the drop-in host-pointer API, timed with
     the reference protocol (shortened): what benchmark.sh would run."""

@@ -22,7 +22,14 @@ counter.
 The test runs it to the end as a child process and requires "[OK] All
 validation tests passed!" for all five cases, no "[ERROR]" line, exit status
 0, "ALL BENCHMARKS COMPLETED" and, parsed by harness/out2csv.py, the six
-legacy timing lines of every case.  The reference's single-threaded
+legacy timing lines of every case.  The host API's exact mode (the default,
+DESIGN.md §5) sums every call in gemm_basic's order, so compare() sees zero
+difference.  A failure keeps its evidence: the assertion message carries the
+case header, compare()'s "Error at (row, col) = ... expected ... got" line
+(dense.c:50-53) and the library's $TCSC_HOST_PATHS lines (which builder made
+W and which path and K-split each variant took).  It runs after every other
+GPU test (tests/conftest.py): it is a long end-to-end run, and under -x a red
+here must not hide the per-row parity tests.  The reference's single-threaded
 gemm_basic is timed >= 50 times per case (main.cpp:54-113), so the run takes
 a few minutes; the output is streamed into gpurun_out/main_amd_out.txt as it
 arrives when that directory exists (profiles/ holds a committed copy per
@@ -40,7 +47,7 @@ import pytest
 
 from conftest import PKG, ROOT
 
-pytestmark = [pytest.mark.gpu, pytest.mark.config_parity]
+pytestmark = [pytest.mark.gpu, pytest.mark.run_last]
 
 BIN = os.path.join(ROOT, "oracle", "_ref", "main_amd_rv")
 CASES = [(1, 512, 2048), (1, 1024, 4096), (1, 2048, 8192), (256, 512, 2048), (256, 1024, 4096)]
@@ -58,6 +65,9 @@ def test_reference_main_cpp_validates_every_case():
     env = dict(os.environ)
     env.pop("TCSC_PATH", None)
     env["TCSC_DENSE_THREADS"] = "0"  # the timing calls' gemm_basic on the box's cores
+    env["TCSC_HOST_PATHS"] = "1"  # one line per matrix and variant: builder, path, K-split
+    for k in ("TCSC_HOST_FAST", "TCSC_ORDER", "TCSC_SLICES", "TCSC_SHARD_AXIS"):
+        env.pop(k, None)
     live = None
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
         live = open(os.path.join(ROOT, "gpurun_out", "main_amd_out.txt"), "w", buffering=1)
@@ -76,7 +86,7 @@ def test_reference_main_cpp_validates_every_case():
     p = subprocess.Popen([BIN], stdin=subprocess.DEVNULL, stdout=slave, stderr=slave, cwd=ROOT, env=env,
                          start_new_session=True)
     os.close(slave)
-    lines, oks, errors = [], 0, []
+    lines, oks, errors, evidence = [], 0, [], []
     t0 = beat = time.time()
     buf = b""
 
@@ -91,6 +101,8 @@ def test_reference_main_cpp_validates_every_case():
                 live.write(line + "\n")
             if "[ERROR]" in line:
                 errors.append(line.strip())
+            if "Error at (row, col)" in line or "[TEST " in line or "[tcsc_amd]" in line:
+                evidence.append(line.strip())
             if OK in line:
                 oks += 1
                 if live:
@@ -124,8 +136,9 @@ def test_reference_main_cpp_validates_every_case():
             live.write(f"# rc={p.returncode} after {time.time() - t0:.1f} s\n")
             live.close()
     out = "\n".join(lines) + "\n"
-    assert not errors, errors
-    assert oks == len(CASES), f"{oks} of {len(CASES)} cases validated; rc={p.returncode}\n{out[-3000:]}"
+    assert not errors, "\n".join(errors + ["-- evidence (case headers, compare(), paths):"] + evidence[-60:])
+    assert oks == len(CASES), (f"{oks} of {len(CASES)} cases validated; rc={p.returncode}\n" +
+                               "\n".join(evidence[-60:]) + "\n" + out[-3000:])
     assert p.returncode == 0 and "ALL BENCHMARKS COMPLETED" in out, out[-3000:]
     tag = "[harness_wrap] gemm_basic:"
     report = [ln[ln.index(tag) + len(tag):].strip() for ln in lines if tag in ln]  # (after a progress bar)

@@ -162,6 +162,7 @@ def _arrays(g):
 
 
 @pytest.mark.gpu
+@pytest.mark.config_parity
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
 def test_sparse_gemm_fast_order_within_bound(gpu, oracle, name):
     g = load_golden(name)
@@ -179,6 +180,7 @@ def test_sparse_gemm_fast_order_within_bound(gpu, oracle, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.config_parity
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
 def test_sparse_gemm_reference_order_bit_exact(gpu, name):
     """TCSC_ORDER_REFERENCE: y = 0 + sum(+1) - sum(-1) + b in SparseGEMM.h's
@@ -195,6 +197,7 @@ def test_sparse_gemm_reference_order_bit_exact(gpu, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.config_parity
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
 def test_dense_gemm_matches_reference_gemm(gpu, name):
     g = load_golden(name)
@@ -256,13 +259,19 @@ def test_reference_sparsegemm_harness_passes(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.config_parity
 @pytest.mark.parametrize("seed", range(6))
-def test_raw_api_matches_device_plan_and_oracle(gpu, oracle, seed):
+def test_raw_api_matches_device_plan_and_oracle(gpu, oracle, seed, monkeypatch):
     """Seeded random shapes: the raw host API (SparseGEMM.h path) against the
-    device API with TCSC_VARIANT_SPARSE_GEMM (bit for bit: same plan, same
-    order) and against the fp64 oracle (bound); integer inputs bit-exact with
-    the oracle's a8 restatement (SparseGEMM.h:104-119)."""
+    device API with TCSC_VARIANT_SPARSE_GEMM (bit for bit: the host API's
+    exact mode is the device API's gather with K unsplit) and against the
+    fp64 oracle (bound); integer inputs bit-exact with the oracle's a8
+    restatement (SparseGEMM.h:104-119)."""
     import torch
+
+    monkeypatch.delenv("TCSC_HOST_FAST", raising=False)
+    monkeypatch.setenv("TCSC_PATH", "gather")
+    monkeypatch.setenv("TCSC_SLICES", "1")
 
     rng = np.random.default_rng(1000 + seed)
     M = int(rng.choice([1, 3, 17, 64, 300, 1024]))

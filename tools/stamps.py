@@ -33,6 +33,7 @@ ap.add_argument("--lib", default=os.path.join(PKG, "lib", "abl", "libtcsc_amd_st
 args = ap.parse_args()
 cfg_idx = args.cfg_pos if args.cfg_pos is not None else args.cfg
 os.environ["TCSC_AMD_LIB"] = args.lib
+os.environ["TCSC_ALLOW_DIAG"] = "1"  # the stamps build is diagnostic
 sys.path.insert(0, PKG)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

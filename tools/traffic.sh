@@ -18,7 +18,7 @@ for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
 done
 ABL=${ABL_LIB:-$PWD/sparse-matrix-multiplication-benchmark_amd/lib/abl/libtcsc_amd_abl0_nd.so}
 rm -rf ${T}4
-TCSC_AMD_LIB=$ABL timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d ${T}4 -o run -- $B --no-validate > ${T}4.log 2>&1
+TCSC_ALLOW_DIAG=1 TCSC_AMD_LIB=$ABL timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d ${T}4 -o run -- $B --no-validate > ${T}4.log 2>&1
 rc=$?; echo "pass 4 (FETCH_SIZE, no-DMA ablation) rc=$rc"; [ $rc -ne 0 ] && exit $rc
 # profiles/traffic.json: run `python tools/traffic_json.py` after gpurun merged gpurun_out/ back
 exit 0
