@@ -77,9 +77,11 @@ typedef struct {
     int n_chunks;        /* ceil(K / chunk_k)                             */
     size_t device_bytes; /* HBM held by the plan                          */
     int order;           /* enum tcsc_order the plan was built for        */
-    int mfma_min_M;      /* > 0: the plan holds the MFMA image of W (near-
-                            dense W, see tcsc_gpu_sgemm) and launches with
-                            M >= mfma_min_M use it; 0: gather only        */
+    int mfma_min_M;      /* > 0: the plan holds the MFMA image of W (denser
+                            W, see tcsc_gpu_sgemm) and launches with
+                            M >= mfma_min_M may use it (the cost model;
+                            tcsc_gpu_launch_info says which path a given
+                            M takes); 0: gather only                      */
 } tcsc_gpu_plan_info;
 
 /* Number of HIP devices visible (0 when there is no GPU). */
@@ -164,8 +166,10 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan *plan);
  * Asynchronous on `stream`; once the workspace covers M (see
  * tcsc_gpu_plan_reserve) no allocation and no synchronisation (safe to
  * capture in a hipGraph).
- * Near-dense W (density >= 0.2, see tcsc_gpu_plan_info.mfma_min_M): launches
- * with M >= mfma_min_M run the MFMA path -- X split exactly into three bf16
+ * Denser W (density >= 0.06, see tcsc_gpu_plan_info.mfma_min_M): launches
+ * with M >= mfma_min_M run the MFMA path where a per-launch cost model says
+ * it beats the gather (measured crossover ~0.08 at M >= 2048, ~0.25 at
+ * M <= 256 for K = N = 8192) -- X split exactly into three bf16
  * parts (k_split3) and one bf16 GEMM with fp32 accumulation against the
  * plan's bf16 image of W on the matrix cores (k_gemm3, the library's own
  * gfx950 kernel, bias and PReLU fused in its store), then the exact fixup of

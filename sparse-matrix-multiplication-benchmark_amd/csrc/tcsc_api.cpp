@@ -225,12 +225,14 @@ int current_order() {
 // ---- MFMA path selection ----------------------------------
 // $TCSC_PATH at plan creation: "gather" never builds the MFMA image, "mfma"
 // builds it for any W and uses it for every M, anything else (default)
-// builds it when the density reaches kMfmaDensity and uses it for
-// M >= kMfmaMinM.  The crossover (cfg 5 measurements): the gather runs
-// ~27 T adds/s near density 0.5, the bf16 x3 GEMM ~1.7 PFLOP/s = 6 flops
-// per (m, k, n), i.e. it wins above density ~0.1; 0.2 leaves a 2x margin
-// for smaller, less efficient GEMM shapes.
-constexpr double kMfmaDensity = 0.2;
+// builds it when the density reaches kMfmaDensity, and a launch with
+// M >= kMfmaMinM takes it where mfma_cheaper() says the GEMM is faster.
+// Measured crossover (round 6, tools/crossover.py, profiles/r06_crossover.txt):
+// at M = 2048 / 4096 the GEMM wins from density ~0.08; at M <= 256 (K = N =
+// 8192), where its grid is small and every workgroup walks all of K, only
+// from ~0.25.  The image is therefore built from density 0.06 and the choice
+// is made per launch by the cost model below, fitted to those measurements.
+constexpr double kMfmaDensity = 0.06;
 constexpr int kMfmaMinM = 64;
 constexpr double kMfmaMaxImageBytes = 16.0 * (1ull << 30);  // build: fp32 scratch + the bf16 W^T, 6 B a cell
 
@@ -253,7 +255,27 @@ size_t mfma_ws_bytes(int M, int K) { return align256((size_t)M * tcsc::mfma_ldk(
 bool valid_variant(int v) { return v >= TCSC_VARIANT_BASIC && v <= TCSC_VARIANT_SPARSE_GEMM; }
 bool is_prelu(int v) { return v >= TCSC_VARIANT_PRELU_BASIC && v <= TCSC_VARIANT_PRELU_ONTHEGO; }
 
-bool use_mfma(const tcsc_gpu_plan* p, int M) { return p->wt && M >= p->mfma_min_M && p->rows > 0; }
+// Per-launch cost model (microseconds), fitted to tools/crossover.py on the
+// box (profiles/r06_crossover.txt):
+//  * gather: ~20 us fixed + one add per nonzero and row of the 256-row tiles
+//    it runs (M rounded up to 256) at ~23 T adds/s;
+//  * MFMA: ~15 us fixed (k_split3, k_fixup, launches) + the larger of the
+//    bf16 x3 GEMM's 6 flops per (m, k, n) at ~1.5 PFLOP/s and the K walk
+//    every workgroup makes when the grid is small (~24 ns per k).
+// Within ~5 % of the measured times near the crossover, where either choice
+// costs about the same.
+bool mfma_cheaper(const tcsc_gpu_plan* p, int M) {
+    const double nnz = (double)(p->n_pos + p->n_neg), Kb = (double)tcsc::mfma_ldw(p->rows);
+    const double Mp = (double)(((long long)M + tcsc::kTM - 1) / tcsc::kTM * tcsc::kTM);
+    const double gather_us = 20.0 + Mp * nnz / 23.0e6;
+    const double mfma_us = 15.0 + std::max(6.0 * M * Kb * p->cols / 1.5e9, Kb * 0.0244);
+    return mfma_us < gather_us;
+}
+
+// forced (TCSC_PATH=mfma: mfma_min_M 1): every launch; default: by the cost model
+bool use_mfma(const tcsc_gpu_plan* p, int M) {
+    return p->wt && M >= p->mfma_min_M && p->rows > 0 && (p->mfma_min_M == 1 || mfma_cheaper(p, M));
+}
 
 rocblas_handle rocblas_for_device(int dev) {
     static std::mutex mu;
