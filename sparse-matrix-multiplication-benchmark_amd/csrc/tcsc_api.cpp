@@ -1173,7 +1173,8 @@ int shard_axis() {
 // whose bf16 x3 sums are rounded in its own blocked order.
 // The outputs are then gemm_basic's bits (+ PReLU) on every shape, shard count
 // and shard axis.  With TCSC_HOST_FAST=1 host calls take the device API's
-// fastest paths (MFMA at density >= 0.2, split K): within the fp32 bound.
+// fastest paths (the MFMA path where the cost model picks it, split K): within
+// the fp32 bound.
 bool host_exact() {
     const char* e = std::getenv("TCSC_HOST_FAST");
     return !(e && std::atoi(e) != 0);

@@ -1,8 +1,8 @@
 """The MFMA path for near-dense W (csrc/tcsc_mfma.hip).
 
-Plans of W with density >= 0.2 also hold W as bf16 and launches with
-M >= 64 run Y = [h|m|l] . [W;W;W] on the matrix cores (x = h + m + l split
-exactly into bf16 parts).  Same bars as the gather:
+Plans of W with density >= 0.06 also hold W as bf16, and launches with
+M >= 64 where the per-launch cost model picks it run Y = [h|m|l] . [W;W;W]
+on the matrix cores (x = h + m + l split exactly into bf16 parts).  Same bars as the gather:
 float outputs within 2^-20 * (|b| + sum|x|) of the exact fp64 sums, integer
 inputs bit-exact with the reference's outputs for all five variants, and
 the rows the split cannot carry (inf / NaN / tiny x) recomputed in the

@@ -74,7 +74,7 @@ def test_host_api_is_gemm_basic_bit_for_bit(gpu, oracle, dense_ref, monkeypatch,
 
 def test_host_fast_mode_takes_mfma_within_bound(gpu, oracle, monkeypatch):
     """TCSC_HOST_FAST=1: main.cpp's largest case goes to the MFMA path (as the
-    device API's plans do at density >= 0.2, M >= 64): within the fp32 bound,
+    device API's plans do there by the cost model): within the fp32 bound,
     and the exact mode's cache entry is not reused for it."""
     import torch
 
