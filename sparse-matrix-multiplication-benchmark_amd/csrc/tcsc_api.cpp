@@ -60,10 +60,10 @@ struct tcsc_gpu_plan {
     int order = TCSC_ORDER_FAST;
     tcsc_gpu_plan* chain_pos = nullptr;
     tcsc_gpu_plan* chain_neg = nullptr;
-    // MFMA path for near-dense W (tcsc_mfma.hip): W^T with
-    // three bf16 copies per column (cols x mfma_ldk(rows)), and the column
-    // range's rebased CSC for the rows the bf16 split of X cannot carry.
-    // Launches with M >= mfma_min_M take it; null when the plan is gather-only.
+    // MFMA path for denser W (tcsc_mfma.hip): W^T in bf16,
+    // stored once (cols x mfma_ldw(rows)); the rows the bf16 split of X
+    // cannot carry are recomputed from the CSC copy below.  Launches with
+    // M >= mfma_min_M may take it (use_mfma); null when the plan is gather-only.
     uint16_t* wt = nullptr;
     size_t mfma_bytes = 0;
     // the column range's rebased CSC (fast-order plans): the small-M path
@@ -130,11 +130,17 @@ int device_count_raw() {
     return n;
 }
 
+// a plan under construction: released through tcsc_gpu_plan_destroy, so an
+// early error return frees what was already allocated
+struct PlanDeleter {
+    void operator()(tcsc_gpu_plan* p) const { tcsc_gpu_plan_destroy(p); }
+};
+
 // Build a plan from device-resident TCSC arrays (absolute offsets).
 int build_plan(int rows, int col_begin, int ncols, long long n_pos, long long n_neg, const int* csp,
                const int* csn, const int* rip, const int* rin, int device, hipStream_t st,
                tcsc_gpu_plan** out) {
-    auto plan = std::make_unique<tcsc_gpu_plan>();
+    std::unique_ptr<tcsc_gpu_plan, PlanDeleter> plan(new tcsc_gpu_plan());
     plan->device = device;
     plan->rows = rows;
     plan->cols = ncols;
