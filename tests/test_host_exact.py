@@ -100,3 +100,39 @@ def test_host_fast_mode_takes_mfma_within_bound(gpu, oracle, monkeypatch):
         assert ok, ratio
     W.free()
     tcsc_amd.cache_clear()
+
+
+@pytest.mark.parametrize("i", range(12))
+def test_host_exact_fuzz_shapes_and_shards(gpu, oracle, dense_ref, monkeypatch, i):
+    """Seeded random shapes, densities, shard counts and shard axes through
+    the host API: every variant equals gemm_basic (+ PReLU) bit for bit on
+    finite float inputs, whatever path (small-M, gather) and block split each
+    call takes.  (On non-finite X the two differ by design: gemm_basic forms
+    inf * 0 = NaN for W's zeros, which the TCSC kernels, the reference's
+    included, never read.)"""
+    for k in ("TCSC_HOST_FAST", "TCSC_PATH", "TCSC_SLICES", "TCSC_ORDER"):
+        monkeypatch.delenv(k, raising=False)
+    gemm_basic, src = dense_ref
+    rng = np.random.default_rng(4100 + i)
+    M = int(rng.choice([1, 2, 3, 4, 7, 64, 130, 257, 300]))
+    K = int(rng.integers(1, 2000))
+    N = int(rng.integers(1, 520))
+    density = float(rng.choice([0.01, 0.05, 0.2, 0.5, 0.9]))
+    shards = int(rng.integers(1, 4))
+    axis = str(rng.choice(["cols", "rows"]))
+    monkeypatch.setenv("TCSC_SHARD_AXIS", axis)
+    Wd = oracle.ternary((K, N), density, 4200 + i)
+    X, B = oracle.uniform((M, K), 4300 + i), oracle.uniform((N,), 4400 + i)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    ref = gemm_basic(X, Wd, B)
+    ref_p = pyoracle.prelu(ref, 0.2)
+    tcsc_amd.set_num_shards(shards)
+    try:
+        for variant in pyoracle.VARIANTS:
+            Y = tcsc_amd.sgemm(variant, X, W, B, 0.2)
+            want = ref_p if variant in pyoracle.PRELU_VARIANTS else ref
+            d = _first_diff(Y, want)
+            assert d is None, f"{M}x{K}x{N} d={density} {shards} {axis} blocks, {variant} vs {src}: {d}"
+    finally:
+        tcsc_amd.set_num_shards(0)
+    W.free()
