@@ -109,6 +109,15 @@ def test_device_count_without_gpu_is_zero_or_more(built_lib):
     assert tcsc_amd.device_count() >= 0
 
 
+def test_product_library_is_not_a_diagnostic_build(built_lib):
+    """tcsc_gpu_build_flags() is 0 for the product build; tcsc_amd refuses a
+    nonzero one (the timing-only ablation / stamps / trace builds of
+    tools/ab.mk) unless TCSC_ALLOW_DIAG=1."""
+    assert built_lib.tcsc_gpu_build_flags() == 0
+    src = open(os.path.join(PKG, "tcsc_amd", "__init__.py")).read()
+    assert 'os.environ.get("TCSC_ALLOW_DIAG") != "1"' in src
+
+
 def test_plan_create_rejects_bad_range(built_lib):
     g = load_golden("cfg1")
     W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
