@@ -116,7 +116,7 @@ int tcsc_gpu_plan_get_info(const tcsc_gpu_plan *plan, tcsc_gpu_plan_info *info);
  * aligned, the plan's reserved workspace and the current environment):
  *   TCSC_PATH_GATHER k_transpose + k_stream (+ k_reduce, or the in-launch
  *                    combine: tcsc_gpu_launch_combine)
- *   TCSC_PATH_MFMA   k_split3 + k_gemm3 (+ k_fixup), near-dense W
+ *   TCSC_PATH_MFMA   k_split3 + k_gemm3 (+ k_fixup), denser W (the cost model)
  *   TCSC_PATH_SMALL  k_small_m, M <= 4 (X and -X fit the LDS)
  * and *slices = the K split of the gather paths (1 = none). */
 enum tcsc_path {
