@@ -116,9 +116,12 @@ int tcsc_gpu_plan_get_info(const tcsc_gpu_plan *plan, tcsc_gpu_plan_info *info);
  * aligned, the plan's reserved workspace and the current environment):
  *   TCSC_PATH_GATHER k_transpose + k_stream (+ k_reduce, or the in-launch
  *                    combine: tcsc_gpu_launch_combine)
- *   TCSC_PATH_MFMA   k_split3 + k_gemm3 (+ k_fixup), denser W (the cost model)
+ *   TCSC_PATH_MFMA   k_split3 + k_gemm3 (+ k_reduce4 when K is split,
+ *                    + k_fixup), denser W (the cost model)
  *   TCSC_PATH_SMALL  k_small_m, M <= 4 (X and -X fit the LDS)
- * and *slices = the K split of the gather paths (1 = none). */
+ * and *slices = the K split (1 = none): the gather's, or the MFMA GEMM's on
+ * grids of few 128 x 128 tiles (M <= 256 at N = 8192: partial sums of whole
+ * 64-k blocks, added in slice order). */
 enum tcsc_path {
     TCSC_PATH_GATHER = 0,
     TCSC_PATH_FUSED = 1, /* retired (round 5): the persistent k_fused left the library; never returned */

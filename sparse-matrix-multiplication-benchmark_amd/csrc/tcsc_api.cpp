@@ -252,8 +252,11 @@ int path_mode() {  // 0 auto, 1 gather only, 2 mfma forced
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// workspace of one MFMA launch: X3 (M x mfma_ldk(K) bf16) + M row flags
-size_t mfma_ws_bytes(int M, int K) { return align256((size_t)M * tcsc::mfma_ldk(K) * 2) + (size_t)M * sizeof(int); }
+// workspace of one MFMA launch: X3 (M x mfma_ldk(K) bf16), M row flags, and
+// the split-K slabs of a small grid (tcsc::mfma_slices; none for big tiles)
+size_t mfma_flags_off(int M, int K) { return align256((size_t)M * tcsc::mfma_ldk(K) * 2); }
+size_t mfma_slabs_off(int M, int K) { return mfma_flags_off(M, K) + align256((size_t)M * sizeof(int)); }
+size_t mfma_ws_bytes(int M, int K, int N) { return mfma_slabs_off(M, K) + tcsc::mfma_slab_bytes(M, N, K); }
 
 // Variants 0-4 are the tcsc_sgemm_* family (sparse/tcsc.h); 5 is
 // SparseGEMM.h's sparseGEMM<float> (bias last, no activation).  Bias first
@@ -262,19 +265,24 @@ bool valid_variant(int v) { return v >= TCSC_VARIANT_BASIC && v <= TCSC_VARIANT_
 bool is_prelu(int v) { return v >= TCSC_VARIANT_PRELU_BASIC && v <= TCSC_VARIANT_PRELU_ONTHEGO; }
 
 // Per-launch cost model (microseconds), fitted to tools/crossover.py on the
-// box (profiles/r06_crossover.txt):
+// box (profiles/r06_crossover.txt, r06_crossover_split.txt):
 //  * gather: ~20 us fixed + one add per nonzero and row of the 256-row tiles
 //    it runs (M rounded up to 256) at ~23 T adds/s;
 //  * MFMA: ~15 us fixed (k_split3, k_fixup, launches) + the larger of the
-//    bf16 x3 GEMM's 6 flops per (m, k, n) at ~1.5 PFLOP/s and the K walk
-//    every workgroup makes when the grid is small (~24 ns per k).
-// Within ~5 % of the measured times near the crossover, where either choice
-// costs about the same.
+//    bf16 x3 GEMM's 6 flops per (m, k, n) at ~1.5 PFLOP/s and the K walk of
+//    one workgroup (~24 ns per k, the slice's share when K is split; x1.5
+//    with two workgroups per CU), + for a split K the slab reduce (~3 us +
+//    the slabs read and Y written at ~4 TB/s).
+// Within ~5-10 % of the measured times near the crossover, where either
+// choice costs about the same.
 bool mfma_cheaper(const tcsc_gpu_plan* p, int M) {
     const double nnz = (double)(p->n_pos + p->n_neg), Kb = (double)tcsc::mfma_ldw(p->rows);
     const double Mp = (double)(((long long)M + tcsc::kTM - 1) / tcsc::kTM * tcsc::kTM);
     const double gather_us = 20.0 + Mp * nnz / 23.0e6;
-    const double mfma_us = 15.0 + std::max(6.0 * M * Kb * p->cols / 1.5e9, Kb * 0.0244);
+    const int s = tcsc::mfma_slices(M, p->cols, p->rows);
+    const double walk_us = Kb * 0.0244 / s * (tcsc::mfma_tiles(M, p->cols) * s > 256 ? 1.5 : 1.0);
+    const double reduce_us = s > 1 ? 3.0 + (s + 1.0) * M * p->cols * 4.0 / 4.0e6 : 0.0;
+    const double mfma_us = 15.0 + std::max(6.0 * M * Kb * p->cols / 1.5e9, walk_us) + reduce_us;
     return mfma_us < gather_us;
 }
 
@@ -476,7 +484,7 @@ int combine_giveup_knob() {
 
 // Workspace of one call = [X^T: xt_bytes(M, K)] [split-K slabs, if any].
 size_t wanted_workspace(const tcsc_gpu_plan* p, int M) {
-    if (use_mfma(p, M)) return mfma_ws_bytes(M, p->rows);
+    if (use_mfma(p, M)) return mfma_ws_bytes(M, p->rows, p->cols);
     if (use_small(p, M)) return align256((size_t)M * p->rows * sizeof(float));  // staged X (prepare_x)
     const int s = tcsc::choose_slices(M, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
                                       slices_override());
@@ -599,18 +607,20 @@ namespace {
 int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* dY, int M, int ldy, int variant,
                float a, void* stream, float* ws, size_t ws_bytes, int stage) {
     const int K = p->rows, N = p->cols, ldk = tcsc::mfma_ldk(K);
-    const size_t need = mfma_ws_bytes(M, K);
+    const size_t need = mfma_ws_bytes(M, K, N);
     if (!ws || ws_bytes < need) {
         set_error("tcsc_gpu_sgemm: workspace of %zu bytes < %zu needed for M=%d", ws ? ws_bytes : (size_t)0, need, M);
         return TCSC_E_ARG;
     }
     hipStream_t st = static_cast<hipStream_t>(stream);
     uint16_t* x3 = reinterpret_cast<uint16_t*>(ws);
-    int* flags = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + align256((size_t)M * ldk * 2));
+    int* flags = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + mfma_flags_off(M, K));
+    float* slabs = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + mfma_slabs_off(M, K));
     if (stage != 2) HIP_TRY(tcsc::mfma_split_x(dX, M, K, x3, ldk, flags, st));
     if (stage == 1) return TCSC_OK;
     const bool prelu = is_prelu(variant);
-    HIP_TRY(tcsc::mfma_gemm3(x3, ldk, p->wt, tcsc::mfma_ldw(K), K, M, N, dB, dY, ldy, prelu, a, st));
+    HIP_TRY(tcsc::mfma_gemm3(x3, ldk, p->wt, tcsc::mfma_ldw(K), K, M, N, dB, dY, ldy, prelu, a, slabs,
+                             ws_bytes - mfma_slabs_off(M, K), st));
     // fast order: bias after the sum for every variant
     HIP_TRY(tcsc::mfma_fixup(x3, M, K, ldk, p->ccq, p->crq, N, dB, dY, ldy, false, prelu, a, flags, st));
     return TCSC_OK;
@@ -910,6 +920,11 @@ int tcsc_gpu_plan_reserve(tcsc_gpu_plan* p, int max_M) {
         const int s = tcsc::choose_slices(max_M, p->cols, p->rows, p->n_pos + p->n_neg, p->n_groups, (size_t)-1,
                                           slices_override());
         want = std::max(want, tcsc::xt_bytes(max_M, p->rows) + tcsc::workspace_bytes(max_M, p->cols, s));
+        // the MFMA path at any M <= max_M: its split-K slabs (slices x M x N)
+        // peak at the top row of some count of 128-row tiles
+        want = std::max(want, mfma_ws_bytes(max_M, p->rows, p->cols));
+        for (long long m = 128; m - 127 <= max_M; m += 128)
+            want = std::max(want, mfma_ws_bytes((int)std::min<long long>(m, max_M), p->rows, p->cols));
     }
     if (!p->csync && p->rows > 0 && p->order == TCSC_ORDER_FAST) {
         DeviceGuard dg(p->device);
@@ -941,6 +956,7 @@ int tcsc_gpu_launch_info(const tcsc_gpu_plan* p, int M, int* path, int* slices) 
     *slices = 1;
     if (use_mfma(p, M)) {
         *path = TCSC_PATH_MFMA;
+        *slices = tcsc::mfma_slices(M, p->cols, p->rows);
         return TCSC_OK;
     }
     if (use_small(p, M)) {

@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <type_traits>
 
 #include "tcsc_internal.h"
@@ -281,7 +282,7 @@ __device__ __forceinline__ void gemm3_tile(int tiles_m, int tiles_n, int gm, int
 // The k_gemm3 epilogue (both staging forms): Y = act(acc + bias) for the
 // workgroup's tile, the raw sums parked in the LDS (LDSB bytes, free once the
 // k loop has drained) and stored as whole rows.
-template <int WM, int WN, int FI, int FJ, bool PRELU, int LDSB>
+template <int WM, int WN, int FI, int FJ, bool PRELU, bool BIAS, int LDSB>
 __device__ __forceinline__ void gemm3_store(const f32x4 (&acc)[FI][FJ], char* lds, int lane, int wr, int wc, int m0,
                                             int n0, int M, int N, const float* __restrict__ bias,
                                             float* __restrict__ Y, int ldy, float a) {
@@ -300,9 +301,10 @@ __device__ __forceinline__ void gemm3_store(const f32x4 (&acc)[FI][FJ], char* ld
     float* stg = reinterpret_cast<float*>(lds);
     const bool vec = (ldy & 3) == 0 && (reinterpret_cast<uintptr_t>(Y) & 15) == 0;
     const int c4 = 4 * (threadIdx.x % LPR), col = n0 + c4;
-    f32x4 bq;
+    f32x4 bq = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (BIAS)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) bq[u] = col + u < N ? bias[col + u] : 0.0f;
+        for (int u = 0; u < 4; ++u) bq[u] = col + u < N ? bias[col + u] : 0.0f;
 #pragma unroll
     for (int p = 0; p < TM / PR; ++p) {
 #pragma unroll
@@ -324,7 +326,7 @@ __device__ __forceinline__ void gemm3_store(const f32x4 (&acc)[FI][FJ], char* ld
             f32x4 v = *reinterpret_cast<const f32x4*>(stg + r * SROW + c4);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                v[u] = v[u] + bq[u];
+                if (BIAS) v[u] = v[u] + bq[u];
                 if (PRELU) v[u] = (v[u] < 0.0f) ? a * v[u] : v[u];
             }
             float* dst = Y + (size_t)row * ldy + col;
@@ -340,11 +342,16 @@ __device__ __forceinline__ void gemm3_store(const f32x4 (&acc)[FI][FJ], char* ld
     }
 }
 
-template <int WM, int WN, int FI, int FJ, bool PRELU>
+// PARTIAL (split-K, blockIdx.y = the slice): the workgroup walks 64-k blocks
+// [y * bps, min(nblk, (y + 1) * bps)) and stores its raw fp32 sums into slab
+// y of Y (M x ldy floats per slab); k_reduce4 adds the slabs in slice order,
+// then the bias and the PReLU.
+template <int WM, int WN, int FI, int FJ, bool PRELU, bool PARTIAL>
 __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                                                       int ldk, int ldw, int M, int N, int nblk,
                                                       const float* __restrict__ bias, float* __restrict__ Y, int ldy,
-                                                      float a, int tiles_m, int tiles_n, int gm) {
+                                                      float a, int tiles_m, int tiles_n, int gm, int bps) {
+    static_assert(!(PARTIAL && PRELU), "a partial slab carries raw sums");
     constexpr int TM = WM * FI * 16, TN = WN * FJ * 16, NW = WM * WN;
     constexpr int PA = TM / 8, PB = TN / 8;  // 1-KiB pieces of a slot
     constexpr int ASLOT = PA * 1024, BSLOT = PB * 1024, BOFF = 2 * ASLOT;
@@ -455,19 +462,23 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
     };
     using with_b = std::integral_constant<int, FI + FJ>;
     using a_only = std::integral_constant<int, FI>;
-    const int last = nblk - 1;
-    dma_a(0, 0, 0);
-    dma_b(0, 0);
+    // this workgroup's 64-k blocks (the host makes every slice non-empty);
+    // ring slots count from the first of them
+    const int b0 = PARTIAL ? (int)blockIdx.y * bps : 0;
+    const int b1 = PARTIAL ? min(nblk, b0 + bps) : nblk;
+    const int last = b1 - 1;
+    dma_a(b0, 0, 0);
+    dma_b(b0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    dma_a(0, 1, 1);
+    dma_a(b0, 1, 1);
     frag_b(0, 0, 0);
     frag_a(0, 0, 0);
-    for (int blk = 0; blk < nblk; ++blk) {
-        const int bs = blk & 1;
+    for (int blk = b0; blk < b1; ++blk) {
+        const int bs = (blk - b0) & 1;
 #pragma unroll
         for (int part = 0; part < 3; ++part) {
-            const int as = (blk + part) & 1;  // (3 * blk + part) & 1
+            const int as = (blk - b0 + part) & 1;  // (3 * (blk - b0) + part) & 1
             if (part == 0) frag_b(1, bs, 1);
             frag_a(1, as, 1);
             mma(0);
@@ -494,7 +505,9 @@ __global__ void __launch_bounds__(WM * WN * 64) k_gemm3(const uint16_t* __restri
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    gemm3_store<WM, WN, FI, FJ, PRELU, 2 * ASLOT + 2 * BSLOT>(acc, lds, lane, wr, wc, m0, n0, M, N, bias, Y, ldy, a);
+    float* out = PARTIAL ? Y + (size_t)blockIdx.y * M * ldy : Y;
+    gemm3_store<WM, WN, FI, FJ, PRELU, !PARTIAL, 2 * ASLOT + 2 * BSLOT>(acc, lds, lane, wr, wc, m0, n0, M, N, bias, out,
+                                                                        ldy, a);
 }
 
 }  // namespace
@@ -552,37 +565,88 @@ hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int
 
 // Tile choice: 128 x 512 (8 waves) unless a grid of 256 x 256 tiles would
 // leave more than half of the 256 CUs idle, then 128 x 128 (4 waves).
+bool mfma_big_tiles(int M, int N) { return (long long)((M + 255) / 256) * ((N + 255) / 256) >= 128; }
+
+// Workgroups of the unsplit grid: 128 x 512 tiles, or 128 x 128 ones.
+long long mfma_tiles(int M, int N) {
+    return mfma_big_tiles(M, N) ? (long long)((M + 127) / 128) * ((N + 511) / 512)
+                                : (long long)((M + 127) / 128) * ((N + 127) / 128);
+}
+
+// Split-K of a grid with fewer tiles than it can run at once: enough slices
+// of the 64-k blocks to bring it to ~512 workgroups of the small tiles (two
+// fit a CU: 64 KiB of LDS, 4 waves each) or ~256 of the large ones (one per
+// CU), each slice at least 8 blocks, at most 16 slices (k_reduce4's limit);
+// normalized so no slice is empty.  Measured (tools/crossover.py, K = N =
+// 8192): M = 64 0.199 -> 0.062 ms, M = 256 0.212 -> 0.108, M = 1024 (large
+// tiles, 2 slices) 0.456 -> 0.32; targets of 768 / 1024 small tiles or 512
+// large ones were slower.  $TCSC_MFMA_WGS overrides the target (A/B; 0 =
+// never split).
+int mfma_split_target(bool big) {
+    const char* e = std::getenv("TCSC_MFMA_WGS");
+    return e ? std::atoi(e) : big ? 256 : 512;
+}
+
+int mfma_slices(int M, int N, int K) {
+    if (M <= 0 || N <= 0) return 1;
+    const long long tiles = mfma_tiles(M, N);
+    const int nblk = mfma_nblk(K);
+    const long long s = std::min<long long>({mfma_split_target(mfma_big_tiles(M, N)) / tiles, 16, nblk / 8});
+    if (s < 2) return 1;
+    const int bps = (int)((nblk + s - 1) / s);
+    return (nblk + bps - 1) / bps;
+}
+
+size_t mfma_slab_bytes(int M, int N, int K) {
+    const int s = mfma_slices(M, N, K);
+    return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
+}
+
 template <bool PRELU>
 static hipError_t launch_gemm3_t(const uint16_t* x3, int ldk, const uint16_t* wt, int ldw, int nblk, int M, int N,
-                                 const float* B, float* Y, int ldy, float a, hipStream_t st) {
-    const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
+                                 const float* B, float* Y, int ldy, float a, float* slabs, int slices,
+                                 hipStream_t st) {
     // bands of 4 row tiles: an XCD's 32 workgroups share 4 A tiles (staged every
     // sub-step) and 8 W tiles (once per block); 8 x 4 was 2 % slower at cfg 5
     constexpr int kGm = 4;
-    if (big >= 128) {
+    if (mfma_big_tiles(M, N)) {
         // 128 x 512 tiles of 8 waves (1 x 8, 128 x 64 each): A, staged every
         // sub-step, is the narrow side (37.3 KiB staged per sub-step, 256 x 256
         // tiles: 42.7; 1.4 % faster at cfg 5).  Its LDS is the whole 160 KiB.
         const int tm = (M + 127) / 128, tn = (N + 511) / 512;
         const int gm = std::min(kGm, tm);
-        hipLaunchKernelGGL((k_gemm3<1, 8, 8, 4, PRELU>), dim3(tm * tn), dim3(512), 0, st, x3, wt, ldk, ldw, M, N, nblk,
-                           B, Y, ldy, a, tm, tn, gm);
+        if (slices <= 1)
+            hipLaunchKernelGGL((k_gemm3<1, 8, 8, 4, PRELU, false>), dim3(tm * tn), dim3(512), 0, st, x3, wt, ldk, ldw,
+                               M, N, nblk, B, Y, ldy, a, tm, tn, gm, nblk);
+        else
+            hipLaunchKernelGGL((k_gemm3<1, 8, 8, 4, false, true>), dim3(tm * tn, slices), dim3(512), 0, st, x3, wt,
+                               ldk, ldw, M, N, nblk, nullptr, slabs, N, 0.0f, tm, tn, gm, (nblk + slices - 1) / slices);
     } else {
         const int tm = (M + 127) / 128, tn = (N + 127) / 128;
         const int gm = std::min(kGm, tm);
-        hipLaunchKernelGGL((k_gemm3<2, 2, 4, 4, PRELU>), dim3(tm * tn), dim3(256), 0, st, x3, wt, ldk, ldw, M, N, nblk,
-                           B, Y, ldy, a, tm, tn, gm);
+        if (slices <= 1)
+            hipLaunchKernelGGL((k_gemm3<2, 2, 4, 4, PRELU, false>), dim3(tm * tn), dim3(256), 0, st, x3, wt, ldk, ldw,
+                               M, N, nblk, B, Y, ldy, a, tm, tn, gm, nblk);
+        else
+            hipLaunchKernelGGL((k_gemm3<2, 2, 4, 4, false, true>), dim3(tm * tn, slices), dim3(256), 0, st, x3, wt,
+                               ldk, ldw, M, N, nblk, nullptr, slabs, N, 0.0f, tm, tn, gm, (nblk + slices - 1) / slices);
     }
-    return hipGetLastError();
+    // split K: raw partial tiles went into slabs[slice] (M x N); then
+    // act(s0 + s1 + ... + b) in slice order by k_reduce4
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess || slices <= 1) return e;
+    return launch_reduce_slabs(slabs, slices, M, N, B, Y, ldy, false, PRELU, a, st);
 }
 
 hipError_t mfma_gemm3(const uint16_t* x3, int ldk, const uint16_t* wt, int ldw, int K, int M, int N, const float* B,
-                      float* Y, int ldy, bool prelu, float a, hipStream_t st) {
+                      float* Y, int ldy, bool prelu, float a, float* slabs, size_t slab_bytes, hipStream_t st) {
     if (M <= 0 || N <= 0) return hipSuccess;
     const int nblk = mfma_nblk(K);
     if (nblk < 1 || ldk != mfma_ldk(K) || ldw != mfma_ldw(K)) return hipErrorInvalidValue;
-    return prelu ? launch_gemm3_t<true>(x3, ldk, wt, ldw, nblk, M, N, B, Y, ldy, a, st)
-                 : launch_gemm3_t<false>(x3, ldk, wt, ldw, nblk, M, N, B, Y, ldy, a, st);
+    const int slices = mfma_slices(M, N, K);
+    if (slices > 1 && (!slabs || slab_bytes < mfma_slab_bytes(M, N, K))) return hipErrorInvalidValue;
+    return prelu ? launch_gemm3_t<true>(x3, ldk, wt, ldw, nblk, M, N, B, Y, ldy, a, slabs, slices, st)
+                 : launch_gemm3_t<false>(x3, ldk, wt, ldw, nblk, M, N, B, Y, ldy, a, slabs, slices, st);
 }
 
 hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cq, const int* crq, int ncols,

@@ -54,12 +54,14 @@ def test_graph_replay_bit_identical(torch_gpu, oracle, M, K, N, density, variant
     W.free()
 
 
-def test_graph_replay_mfma_path_with_and_without_special_rows(torch_gpu, oracle):
+def test_graph_replay_mfma_path_with_and_without_special_rows(torch_gpu, oracle, monkeypatch):
     """the MFMA path's row flags must not carry over between
     replays.  One captured launch, replayed on X holding inf / NaN / tiny
     values (flagged rows, recomputed exactly), then on X without them, then
     with them again: every replay equals the eager launch on the same X, bit
-    for bit."""
+    for bit.  The path is forced (at this size the cost model picks the
+    gather); its grid splits K, so the capture holds k_reduce4 too."""
+    monkeypatch.setenv("TCSC_PATH", "mfma")
     torch = torch_gpu
     dev = torch.device("cuda:0")
     M, K, N = 256, 1024, 512
@@ -75,6 +77,7 @@ def test_graph_replay_mfma_path_with_and_without_special_rows(torch_gpu, oracle)
     plan = tcsc_amd.Plan(W, 0, N, 0, side.cuda_stream)
     plan.reserve(M)
     assert plan.info()["mfma_min_M"] and M >= plan.info()["mfma_min_M"]
+    assert plan.launch_info(M) == ("mfma", 2)
     X = torch.empty((M, K), device=dev)
     eager = {}
     for name, x in (("plain", plain), ("special", special)):

@@ -2,7 +2,11 @@
 
 Plans of W with density >= 0.06 also hold W as bf16, and launches with
 M >= 64 where the per-launch cost model picks it run Y = [h|m|l] . [W;W;W]
-on the matrix cores (x = h + m + l split exactly into bf16 parts).  Same bars as the gather:
+on the matrix cores (x = h + m + l split exactly into bf16 parts).  At the
+small shapes most tests use the cost model prefers the gather, so they force
+the path (TCSC_PATH=mfma) and check the launch took it; grids of few
+128 x 128 tiles split K (whole 64-k blocks per slice, slabs added in slice
+order).  Same bars as the gather:
 float outputs within 2^-20 * (|b| + sum|x|) of the exact fp64 sums, integer
 inputs bit-exact with the reference's outputs for all five variants, and
 the rows the split cannot carry (inf / NaN / tiny x) recomputed in the
@@ -67,6 +71,7 @@ def device_run(W, X, B, variant, a=0.2, ldy=None, c0=0, c1=None, prepared=False)
         plan.sgemm(dX, dB, dY, M, ldy, variant, a)
     torch.cuda.synchronize()
     info = plan.info()
+    info["launch"] = plan.launch_info(M)
     plan.destroy()
     Y = dY.cpu().numpy()
     assert np.all(Y[:, nc:] == 7.0), "columns beyond the plan's were written"
@@ -80,21 +85,21 @@ def float_case(o, M, K, N, density, seed):
 
 @pytest.mark.parametrize("K", [700, 701])
 def test_float_within_bound_all_variants(gpu, oracle, path, K):
-    path(None)
+    path("mfma")
     Wd, X, B = float_case(oracle, 200, K, 300, 0.5, 31)
     W = tcsc_amd.TcscMatrix.from_dense(Wd)
     Wref = oracle.tcsc_from_dense(Wd)
     Y64, S64 = oracle.f64_rows(X, Wref, B)
     for variant in pyoracle.VARIANTS:
         Y, info = device_run(W, X, B, variant)
-        assert info["mfma_min_M"] == 64
+        assert info["launch"] == ("mfma", 1)
         ok, ratio = pyoracle.check_close(Y, Y64, S64, 0.2 if variant in pyoracle.PRELU_VARIANTS else None)
         assert ok, f"{variant}: worst err/bound {ratio:.3g}"
     W.free()
 
 
 def test_integer_inputs_bit_exact(gpu, oracle, path):
-    path(None)
+    path("mfma")
     M, K, N = 130, 512, 257
     Wd = oracle.ternary((K, N), 0.5, 41)
     X, B = oracle.integers((M, K), 42), oracle.integers((N,), 43)
@@ -102,7 +107,7 @@ def test_integer_inputs_bit_exact(gpu, oracle, path):
     Wref = oracle.tcsc_from_dense(Wd)
     for variant in pyoracle.VARIANTS:
         Y, info = device_run(W, X, B, variant)
-        assert info["mfma_min_M"] == 64
+        assert info["launch"][0] == "mfma"
         ref = oracle.sgemm(variant, X, Wref, B, 0.2)
         np.testing.assert_array_equal(Y, ref, err_msg=variant)
         Yh = tcsc_amd.sgemm(variant, X, W, B, 0.2)  # host API: the cached plan takes the same path
@@ -143,9 +148,9 @@ def test_special_rows_match_the_gather_bit_for_bit(gpu, oracle, path, monkeypatc
     X[40, :] = np.float32(1e-38)
     W = tcsc_amd.TcscMatrix.from_dense(Wd)
     for variant in pyoracle.VARIANTS:
-        path(None)
+        path("mfma")
         Ym, info = device_run(W, X, B, variant)
-        assert info["mfma_min_M"] == 64
+        assert info["launch"][0] == "mfma"
         path("gather")
         Yg, info = device_run(W, X, B, variant)
         assert info["mfma_min_M"] == 0
@@ -180,14 +185,14 @@ def test_path_modes_and_small_M(gpu, oracle, path):
     Wd2, X2, B2 = float_case(oracle, 40, 300, 128, 0.6, 62)
     W2 = tcsc_amd.TcscMatrix.from_dense(Wd2)
     Y, info = device_run(W2, X2, B2, "basic")
-    assert info["mfma_min_M"] == 64
+    assert info["mfma_min_M"] == 64 and info["launch"][0] == "gather"
     Y64, S64 = oracle.f64_rows(X2, oracle.tcsc_from_dense(Wd2), B2)
     assert pyoracle.check_close(Y, Y64, S64)[0]
     W2.free()
 
 
 def test_column_block_pitch_and_prepared(gpu, oracle, path):
-    path(None)
+    path("mfma")
     Wd, X, B = float_case(oracle, 256, 512, 400, 0.5, 71)
     W = tcsc_amd.TcscMatrix.from_dense(Wd)
     Wref = oracle.tcsc_from_dense(Wd)
@@ -195,7 +200,7 @@ def test_column_block_pitch_and_prepared(gpu, oracle, path):
     for c0, c1, ldy in ((0, 400, 403), (96, 333, 240), (250, 400, 150)):
         for prepared in (False, True):
             Y, info = device_run(W, X, B, "prelu_separate", c0=c0, c1=c1, ldy=ldy, prepared=prepared)
-            assert info["mfma_min_M"] == 64
+            assert info["launch"][0] == "mfma"
             ok, ratio = pyoracle.check_close(Y, Y64[:, c0:c1], S64[:, c0:c1], 0.2)
             assert ok, f"[{c0},{c1}) ldy={ldy} prepared={prepared}: {ratio:.3g}"
     W.free()
@@ -204,7 +209,7 @@ def test_column_block_pitch_and_prepared(gpu, oracle, path):
 def test_repeated_rows_in_a_column(gpu, oracle, path):
     """A hand-built TCSC whose columns repeat rows (within a sign and across
     signs): every entry counts, as in the reference's loops (tcsc.c:86-93)."""
-    path(None)
+    path("mfma")
     K, N, M = 80, 70, 100
     rng = np.random.default_rng(5)
     cols_p, cols_n = [], []
@@ -221,7 +226,7 @@ def test_repeated_rows_in_a_column(gpu, oracle, path):
     Wref = pyoracle.TCSC(K, N, csp, csn, rip, rin)
     X, B = oracle.integers((M, K), 81), oracle.integers((N,), 82)
     Y, info = device_run(W, X, B, "basic")
-    assert info["mfma_min_M"] == 64
+    assert info["launch"][0] == "mfma"
     np.testing.assert_array_equal(Y, oracle.sgemm("basic", X, Wref, B))
     W.free()
 
@@ -283,6 +288,119 @@ def test_golden_fixtures_forced_mfma(gpu, oracle, path, name):
             Y64, S64 = oracle.f64_rows(g["X"], tcsc_of(g), g["B"])
             ok, ratio = pyoracle.check_close(Y, Y64, S64, a if variant in pyoracle.PRELU_VARIANTS else None)
             assert ok, f"{variant}: worst err/bound {ratio:.3g}"
+    W.free()
+
+
+SPLIT_CASES = [  # (M, K, N): grids of few 128 x 128 tiles, so K is split
+    (64, 4096, 300),    # 3 tiles: 8 slices of 8 blocks
+    (256, 4096, 300),   # 6 tiles: 8 slices
+    (100, 2050, 1000),  # 8 tiles: 4 slices of 9, 9, 9, 6 blocks (a ragged last block)
+    (130, 1024, 257),   # 9 tiles, ragged row and column tiles: 2 slices
+]
+
+
+@pytest.mark.parametrize("case", range(len(SPLIT_CASES)))
+def test_split_k_integer_exact_all_variants(gpu, oracle, path, case):
+    """Split K (k_gemm3 PARTIAL + k_reduce4): integer inputs stay exact, so
+    every variant equals the reference's outputs bit for bit, and the host
+    API's cached plan (fast mode) takes the same split."""
+    path("mfma")
+    M, K, N = SPLIT_CASES[case]
+    Wd = oracle.ternary((K, N), 0.5, 700 + case)
+    X, B = oracle.integers((M, K), 710 + case), oracle.integers((N,), 720 + case)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    Wref = oracle.tcsc_from_dense(Wd)
+    for variant in pyoracle.VARIANTS:
+        Y, info = device_run(W, X, B, variant)
+        assert info["launch"][0] == "mfma" and info["launch"][1] > 1, info["launch"]
+        ref = oracle.sgemm(variant, X, Wref, B, 0.2)
+        np.testing.assert_array_equal(Y.view(np.uint32), ref.view(np.uint32), err_msg=variant)
+    Yh = tcsc_amd.sgemm("prelu_onthego", X, W, B, 0.2)
+    np.testing.assert_array_equal(Yh, oracle.sgemm("prelu_onthego", X, Wref, B, 0.2))
+    W.free()
+
+
+def test_split_k_big_tiles_sampled_rows_integer_exact(gpu, oracle, path):
+    """The large tiles (128 x 512) on a grid of 128 of them (M = 1024,
+    N = 8192: half the CUs) split K in 2 (9 + 9 blocks); integer inputs,
+    sampled rows bit for bit against the reference's outputs."""
+    path("mfma")
+    M, K, N = 1024, 1100, 8192
+    Wd = oracle.ternary((K, N), 0.5, 761)
+    X, B = oracle.integers((M, K), 762), oracle.integers((N,), 763)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    Wref = oracle.tcsc_from_dense(Wd)
+    rows = np.unique(np.concatenate([[0, 127, 128, M - 1], np.random.default_rng(7).integers(0, M, 12)]))
+    for variant in ("basic", "prelu_onthego"):
+        Y, info = device_run(W, X, B, variant)
+        assert info["launch"] == ("mfma", 2), info["launch"]
+        ref = oracle.sgemm(variant, X[rows], Wref, B, 0.2)
+        np.testing.assert_array_equal(Y[rows].view(np.uint32), ref.view(np.uint32), err_msg=variant)
+    W.free()
+
+
+def test_split_k_float_blocks_pitch_prepared(gpu, oracle, path, monkeypatch):
+    """Float inputs through the split GEMM: column blocks (N % 4 != 0 takes
+    k_reduce's scalar form), a row pitch past N, prepare_x + sgemm_prepared;
+    within the fp32 bound, and the unsplit GEMM ($TCSC_MFMA_WGS=0) too."""
+    path("mfma")
+    M, K, N = 96, 3000, 600
+    Wd, X, B = float_case(oracle, M, K, N, 0.4, 731)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    Y64, S64 = oracle.f64_rows(X, oracle.tcsc_from_dense(Wd), B)
+    for wgs in (None, "0"):
+        if wgs is None:
+            monkeypatch.delenv("TCSC_MFMA_WGS", raising=False)
+        else:
+            monkeypatch.setenv("TCSC_MFMA_WGS", wgs)
+        for c0, c1, ldy in ((0, 600, 600), (3, 570, 571), (100, 229, 140)):
+            for prepared in (False, True):
+                Y, info = device_run(W, X, B, "prelu_basic", c0=c0, c1=c1, ldy=ldy, prepared=prepared)
+                assert info["launch"][0] == "mfma"
+                assert (info["launch"][1] > 1) == (wgs is None), info["launch"]
+                ok, ratio = pyoracle.check_close(Y, Y64[:, c0:c1], S64[:, c0:c1], 0.2)
+                assert ok, f"[{c0},{c1}) ldy={ldy} prepared={prepared} wgs={wgs}: {ratio:.3g}"
+    W.free()
+
+
+def test_split_k_special_rows_match_the_gather(gpu, oracle, path, monkeypatch):
+    """Rows the bf16 split cannot carry are rewritten by k_fixup after the
+    slabs are reduced: bit-identical to the unsplit gather."""
+    monkeypatch.setenv("TCSC_SLICES", "1")
+    M, K, N = 70, 2048, 200
+    Wd, X, B = float_case(oracle, M, K, N, 0.3, 741)
+    X[5, 1000] = np.inf
+    X[6, 7] = np.nan
+    X[60, 2047] = np.float32(1e-39)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    path("mfma")
+    Ym, info = device_run(W, X, B, "prelu_onthego")
+    assert info["launch"][0] == "mfma" and info["launch"][1] > 1
+    path("gather")
+    Yg, _ = device_run(W, X, B, "prelu_onthego")
+    flagged = [5, 6, 60]
+    nan = np.isnan(Yg[flagged])
+    assert np.array_equal(np.isnan(Ym[flagged]), nan)
+    np.testing.assert_array_equal(Ym[flagged][~nan].view(np.uint32), Yg[flagged][~nan].view(np.uint32))
+    rest = np.setdiff1d(np.arange(M), flagged)
+    Y64, S64 = oracle.f64_rows(X[rest], oracle.tcsc_from_dense(Wd), B)
+    assert pyoracle.check_close(Ym[rest], Y64, S64, 0.2)[0]
+    W.free()
+
+
+def test_cost_model_takes_the_split_gemm(gpu, oracle, path):
+    """Default plan, M = 256, K = N = 2048 at 50 %: the cost model prefers the
+    split GEMM (4 slices) to the gather; within the bound."""
+    path(None)
+    M, K, N = 256, 2048, 2048
+    Wd, X, B = float_case(oracle, M, K, N, 0.5, 751)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    Y, info = device_run(W, X, B, "basic")
+    assert info["mfma_min_M"] == 64 and info["launch"] == ("mfma", 4), info["launch"]
+    rows = np.arange(0, M, 17)
+    Y64, S64 = oracle.f64_rows(X[rows], oracle.tcsc_from_dense(Wd), B)
+    ok, ratio = pyoracle.check_close(Y[rows], Y64, S64)
+    assert ok, ratio
     W.free()
 
 
