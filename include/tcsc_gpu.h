@@ -147,8 +147,8 @@ int tcsc_gpu_launch_combine(const tcsc_gpu_plan *plan, int M, int *in_launch);
 
 /* Allocate the plan's workspace for launches of up to `max_M` rows: X^T
  * (K x max_M rounded up to 256 floats; the kernel streams X^T rows into LDS)
- * plus, where the cost model splits K over workgroups, the fp32 partial
- * slabs combined in a fixed order.  Optional: tcsc_gpu_sgemm grows the
+ * plus, where the gather's cost model or the MFMA GEMM's grid splits K over
+ * workgroups, the fp32 partial slabs combined in a fixed order.  Optional: tcsc_gpu_sgemm grows the
  * workspace itself on the first call with a larger M (that call then
  * allocates and synchronises the device); reserving up front keeps every
  * sgemm call allocation-free.  Not thread-safe against concurrent launches
@@ -169,13 +169,16 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan *plan);
  * Asynchronous on `stream`; once the workspace covers M (see
  * tcsc_gpu_plan_reserve) no allocation and no synchronisation (safe to
  * capture in a hipGraph).
- * Denser W (density >= 0.06, see tcsc_gpu_plan_info.mfma_min_M): launches
+ * Denser W (density >= 0.055, see tcsc_gpu_plan_info.mfma_min_M): launches
  * with M >= mfma_min_M run the MFMA path where a per-launch cost model says
- * it beats the gather (measured crossover ~0.08 at M >= 2048, ~0.25 at
- * M <= 256 for K = N = 8192) -- X split exactly into three bf16
- * parts (k_split3) and one bf16 GEMM with fp32 accumulation against the
- * plan's bf16 image of W on the matrix cores (k_gemm3, the library's own
- * gfx950 kernel, bias and PReLU fused in its store), then the exact fixup of
+ * it beats the gather (measured crossover ~0.08 at M >= 2048, ~0.04-0.1 at
+ * M <= 256 for K = N = 8192, lower for smaller K and N) -- X
+ * split exactly into three bf16 parts (k_split3) and one bf16 GEMM with fp32
+ * accumulation against the plan's bf16 image of W on the matrix cores
+ * (k_gemm3, the library's own gfx950 kernel, bias and PReLU fused in its
+ * store; a grid with fewer tiles than the chip runs at once splits K into
+ * slices of whole 64-k blocks whose partial sums k_reduce4 adds in slice
+ * order with the bias and PReLU), then the exact fixup of
  * rows holding non-finite or tiny values (k_fixup) -- with the same accuracy
  * bounds as the gather.  It allocates nothing per launch and
  * keeps no state between launches, so graph replays with new X are exact.

@@ -235,10 +235,13 @@ int current_order() {
 // M >= kMfmaMinM takes it where mfma_cheaper() says the GEMM is faster.
 // Measured crossover (round 6, tools/crossover.py, profiles/r06_crossover.txt):
 // at M = 2048 / 4096 the GEMM wins from density ~0.08; at M <= 256 (K = N =
-// 8192), where its grid is small and every workgroup walks all of K, only
-// from ~0.25.  The image is therefore built from density 0.06 and the choice
-// is made per launch by the cost model below, fitted to those measurements.
-constexpr double kMfmaDensity = 0.06;
+// 8192) the unsplit GEMM, whose small grid walked all of K per workgroup,
+// only from ~0.25, and since k_gemm3 splits K over such grids from ~0.04-0.1
+// (profiles/r06_crossover_split.txt).  The image is built from density 0.055
+// (the 0.05 configs, cfg 2/3, stay image-free; a sweep point at 0.06 is not
+// lost to sampling noise under the threshold) and the choice is made per
+// launch by the cost model below, fitted to those measurements.
+constexpr double kMfmaDensity = 0.055;
 constexpr int kMfmaMinM = 64;
 constexpr double kMfmaMaxImageBytes = 16.0 * (1ull << 30);  // build: fp32 scratch + the bf16 W^T, 6 B a cell
 
@@ -265,24 +268,25 @@ bool valid_variant(int v) { return v >= TCSC_VARIANT_BASIC && v <= TCSC_VARIANT_
 bool is_prelu(int v) { return v >= TCSC_VARIANT_PRELU_BASIC && v <= TCSC_VARIANT_PRELU_ONTHEGO; }
 
 // Per-launch cost model (microseconds), fitted to tools/crossover.py on the
-// box (profiles/r06_crossover.txt, r06_crossover_split.txt):
-//  * gather: ~20 us fixed + one add per nonzero and row of the 256-row tiles
+// box (profiles/r06_crossover_split.txt, r06_crossover_small.txt: 120
+// shapes x densities, M = 64 .. 4096, K and N = 256 .. 8192):
+//  * gather: ~38 us fixed + one add per nonzero and row of the 256-row tiles
 //    it runs (M rounded up to 256) at ~23 T adds/s;
-//  * MFMA: ~15 us fixed (k_split3, k_fixup, launches) + the larger of the
+//  * MFMA: ~10 us fixed (k_split3, k_fixup, launches) + the larger of the
 //    bf16 x3 GEMM's 6 flops per (m, k, n) at ~1.5 PFLOP/s and the K walk of
 //    one workgroup (~24 ns per k, the slice's share when K is split; x1.5
 //    with two workgroups per CU), + for a split K the slab reduce (~3 us +
 //    the slabs read and Y written at ~4 TB/s).
-// Within ~5-10 % of the measured times near the crossover, where either
-// choice costs about the same.
+// With these constants the default plan is within 1.02x of the faster
+// forced path at every measured point.
 bool mfma_cheaper(const tcsc_gpu_plan* p, int M) {
     const double nnz = (double)(p->n_pos + p->n_neg), Kb = (double)tcsc::mfma_ldw(p->rows);
     const double Mp = (double)(((long long)M + tcsc::kTM - 1) / tcsc::kTM * tcsc::kTM);
-    const double gather_us = 20.0 + Mp * nnz / 23.0e6;
+    const double gather_us = 38.0 + Mp * nnz / 23.0e6;
     const int s = tcsc::mfma_slices(M, p->cols, p->rows);
     const double walk_us = Kb * 0.0244 / s * (tcsc::mfma_tiles(M, p->cols) * s > 256 ? 1.5 : 1.0);
     const double reduce_us = s > 1 ? 3.0 + (s + 1.0) * M * p->cols * 4.0 / 4.0e6 : 0.0;
-    const double mfma_us = 15.0 + std::max(6.0 * M * Kb * p->cols / 1.5e9, walk_us) + reduce_us;
+    const double mfma_us = 10.0 + std::max(6.0 * M * Kb * p->cols / 1.5e9, walk_us) + reduce_us;
     return mfma_us < gather_us;
 }
 

@@ -25,6 +25,13 @@ def gpu():
     return tcsc_amd.lib()
 
 
+@pytest.fixture(autouse=True)
+def gather_plans(monkeypatch):
+    """These are the gather's combines: plans of the denser shapes (0.1)
+    would otherwise hold the MFMA image and the cost model may take it."""
+    monkeypatch.setenv("TCSC_PATH", "gather")
+
+
 def _plan(torch, K, N, density, seed):
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)

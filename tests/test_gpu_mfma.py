@@ -1,6 +1,6 @@
 """The MFMA path for near-dense W (csrc/tcsc_mfma.hip).
 
-Plans of W with density >= 0.06 also hold W as bf16, and launches with
+Plans of W with density >= 0.055 also hold W as bf16, and launches with
 M >= 64 where the per-launch cost model picks it run Y = [h|m|l] . [W;W;W]
 on the matrix cores (x = h + m + l split exactly into bf16 parts).  At the
 small shapes most tests use the cost model prefers the gather, so they force

@@ -86,8 +86,11 @@ def test_gpu_tcsc_from_dense_bitexact(gpu, name, monkeypatch):
 
 
 def test_device_api_matches_host_api(gpu, torch_cuda, oracle, monkeypatch):
-    """The device API with K unsplit equals the host API's exact mode."""
+    """The device API's gather with K unsplit equals the host API's exact mode
+    (at cfg 1's shape and 10 % density the cost model would otherwise take
+    the MFMA path, which sums in its own order)."""
     monkeypatch.setenv("TCSC_SLICES", "1")
+    monkeypatch.setenv("TCSC_PATH", "gather")
     torch = torch_cuda
     g = load_golden("cfg1")
     W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
@@ -133,10 +136,12 @@ def test_dense_baseline_matches_reference(gpu, torch_cuda, oracle, name):
         check_variant(g, variant, np.ascontiguousarray(out[:, :N]), oracle)
 
 
+@pytest.mark.parametrize("path", ["gather", "mfma"])
 @pytest.mark.parametrize("name", ["cfg1", "edge_k_not_mult4", "edge_long_k"])
-def test_prepare_then_gather_equals_sgemm(gpu, torch_cuda, name):
+def test_prepare_then_gather_equals_sgemm(gpu, torch_cuda, monkeypatch, name, path):
     """tcsc_gpu_prepare_x + tcsc_gpu_sgemm_prepared == tcsc_gpu_sgemm, bit for
-    bit, and one staged X^T serves several gathers."""
+    bit, and one staged X^T (or X3, on the MFMA path) serves several launches."""
+    monkeypatch.setenv("TCSC_PATH", path)
     torch = torch_cuda
     g = load_golden(name)
     W = tcsc_amd.TcscMatrix.from_dense(g["Wd"].astype(np.float32))
@@ -147,6 +152,7 @@ def test_prepare_then_gather_equals_sgemm(gpu, torch_cuda, name):
     stream = torch.cuda.current_stream().cuda_stream
     plan = tcsc_amd.Plan(W, 0, N, 0, stream)
     plan.reserve(M)
+    assert plan.launch_info(M)[0] == (path if path == "mfma" or M > 4 else "small")
     Y1 = torch.empty((M, N), device=dev)
     plan.sgemm(X, B, Y1, M, N, "prelu_basic", 0.2, stream)
     plan.prepare_x(X, M, stream)

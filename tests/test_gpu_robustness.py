@@ -283,7 +283,7 @@ def test_more_than_2pow22_rows_in_one_host_call(gpu, oracle, monkeypatch):
     every sampled row bit-identical to the oracle, ragged last launch too."""
     monkeypatch.setenv("TCSC_HOST_BANDS", "1")
     M, K, N = (1 << 22) + 300, 16, 24
-    Wd = oracle.ternary((K, N), 0.15, 91)  # below the MFMA path's density: the gather
+    Wd = oracle.ternary((K, N), 0.15, 91)  # K < 64: no MFMA image (and the host's exact mode is the gather)
     W = oracle.tcsc_from_dense(Wd)
     Wl = tcsc_amd.TcscMatrix.from_dense(Wd)
     rng = np.random.default_rng(92)
@@ -305,11 +305,13 @@ def test_more_than_2pow22_rows_float_tail_same_order(gpu, oracle, monkeypatch):
     import torch
 
     dev = torch.device("cuda:0")
+    monkeypatch.setenv("TCSC_PATH", "gather")  # the gather's launches (the cost model would take the MFMA path)
     M, K, N, tail = (1 << 22) + 300, 104, 24, 300
     Wd = oracle.ternary((K, N), 0.15, 93)
     Wl = tcsc_amd.TcscMatrix.from_dense(Wd)
     plan = tcsc_amd.Plan(Wl)
     plan.reserve(M)
+    assert plan.launch_info(M)[0] == "gather"
     g = torch.Generator(device=dev)
     g.manual_seed(94)
     X = torch.rand((M, K), generator=g, device=dev) * 2 - 1

@@ -81,6 +81,7 @@ def main():
                 else:
                     os.environ["TCSC_PATH"] = mode
                 plan = tcsc_amd.Plan.from_device(K, N, csp, csn, rip, rin)
+                plan.reserve(M)  # the gather's K split depends on the workspace
                 path, slices = plan.launch_info(M)
                 out[mode + "_path"] = f"{path}/s{slices}"
                 out[mode + "_ms"] = time_plan(plan, X, B, Y, M, N)
