@@ -925,9 +925,10 @@ int tcsc_gpu_plan_reserve(tcsc_gpu_plan* p, int max_M) {
                                           slices_override());
         want = std::max(want, tcsc::xt_bytes(max_M, p->rows) + tcsc::workspace_bytes(max_M, p->cols, s));
         // the MFMA path at any M <= max_M: its split-K slabs (slices x M x N)
-        // peak at the top row of some count of 128-row tiles
+        // peak at the top row of some count of 128-row tiles; from 512 row
+        // tiles on every grid holds at least 512 tiles and never splits
         want = std::max(want, mfma_ws_bytes(max_M, p->rows, p->cols));
-        for (long long m = 128; m - 127 <= max_M; m += 128)
+        for (long long m = 128; m - 127 <= max_M && m <= 512LL * 128; m += 128)
             want = std::max(want, mfma_ws_bytes((int)std::min<long long>(m, max_M), p->rows, p->cols));
     }
     if (!p->csync && p->rows > 0 && p->order == TCSC_ORDER_FAST) {
