@@ -242,7 +242,10 @@ int current_order() {
 // lost to sampling noise under the threshold) and the choice is made per
 // launch by the cost model below, fitted to those measurements.
 constexpr double kMfmaDensity = 0.055;
-constexpr int kMfmaMinM = 64;
+// M <= 4 belongs to the small-M path; from 5 rows on the GEMM's 64 x 256
+// tiles (M <= 64) beat the gather's 256-row tiles wherever the image exists
+// (M = 8 .. 32, K = N = 8192: 1.7-5.3x, profiles/r06_mfma_narrow.txt)
+constexpr int kMfmaMinM = 5;
 constexpr double kMfmaMaxImageBytes = 16.0 * (1ull << 30);  // build: fp32 scratch + the bf16 W^T, 6 B a cell
 
 int path_mode() {  // 0 auto, 1 gather only, 2 mfma forced

@@ -330,6 +330,7 @@ hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int
 // blocks: raw partial sums into `slabs` (mfma_slab_bytes(): slices x M x N
 // floats), added in slice order with the bias and PReLU by k_reduce4.
 bool mfma_big_tiles(int M, int N);
+bool mfma_narrow_tiles(int M, int N);
 long long mfma_tiles(int M, int N);
 int mfma_slices(int M, int N, int K);
 size_t mfma_slab_bytes(int M, int N, int K);

@@ -71,7 +71,11 @@ __device__ inline bool split3(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
 
 // X (M x K, pitch K) -> X3 (M x ldk bf16): [h | m | l | 0 ...] per row, one
 // workgroup per row; flags[row] = 1 when the fixup must recompute the row,
-// else 0 (written every call).
+// else 0 (written every call).  A thread loads kSplitU 16-B pieces before it
+// splits and stores any of them: at small M (one workgroup per row, few rows)
+// the row's loads then overlap instead of running as kq / 256 dependent round
+// trips (M = 64, K = 8192: 11.3 us before).
+constexpr int kSplitU = 8;
 __global__ void __launch_bounds__(256) k_split3(const float* __restrict__ X, int M, int K, uint16_t* __restrict__ X3,
                                                int ldk, int* __restrict__ flags) {
     const int row = blockIdx.x;
@@ -80,24 +84,35 @@ __global__ void __launch_bounds__(256) k_split3(const float* __restrict__ X, int
     const bool vec = (K & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
     bool fix = false;
     const int kq = (K + 3) / 4;
-    for (int q = threadIdx.x; q < kq; q += blockDim.x) {
-        const int k0 = 4 * q;
-        float v[4];
-        if (vec) {
-            typedef float f4 __attribute__((ext_vector_type(4)));
-            const f4 w = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src + k0));
-            v[0] = w.x, v[1] = w.y, v[2] = w.z, v[3] = w.w;
-        } else {
-            for (int j = 0; j < 4; ++j) v[j] = k0 + j < K ? src[k0 + j] : 0.0f;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+    if (vec) {
+        for (int q0 = threadIdx.x; q0 < kq; q0 += kSplitU * blockDim.x) {
+            f4 w[kSplitU];
+#pragma unroll
+            for (int u = 0; u < kSplitU; ++u) {
+                const int q = q0 + u * blockDim.x;
+                if (q < kq) w[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src + 4 * q));
+            }
+#pragma unroll
+            for (int u = 0; u < kSplitU; ++u) {
+                const int q = q0 + u * blockDim.x;
+                if (q >= kq) break;
+                const int k0 = 4 * q;  // k0 .. k0+3 lie in one block
+                uint16_t h[4], m[4], l[4];
+                for (int j = 0; j < 4; ++j) fix |= split3(w[u][j], h[j], m[j], l[j]);
+                *reinterpret_cast<u16x4*>(dst + x3_index(k0, 0)) = u16x4{h[0], h[1], h[2], h[3]};
+                *reinterpret_cast<u16x4*>(dst + x3_index(k0, 1)) = u16x4{m[0], m[1], m[2], m[3]};
+                *reinterpret_cast<u16x4*>(dst + x3_index(k0, 2)) = u16x4{l[0], l[1], l[2], l[3]};
+            }
         }
-        uint16_t h[4], m[4], l[4];
-        for (int j = 0; j < 4; ++j) fix |= split3(v[j], h[j], m[j], l[j]);
-        if (vec) {  // k0 .. k0+3 lie in one block
-            typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
-            *reinterpret_cast<u16x4*>(dst + x3_index(k0, 0)) = u16x4{h[0], h[1], h[2], h[3]};
-            *reinterpret_cast<u16x4*>(dst + x3_index(k0, 1)) = u16x4{m[0], m[1], m[2], m[3]};
-            *reinterpret_cast<u16x4*>(dst + x3_index(k0, 2)) = u16x4{l[0], l[1], l[2], l[3]};
-        } else {
+    } else {
+        for (int q = threadIdx.x; q < kq; q += blockDim.x) {
+            const int k0 = 4 * q;
+            float v[4];
+            for (int j = 0; j < 4; ++j) v[j] = k0 + j < K ? src[k0 + j] : 0.0f;
+            uint16_t h[4], m[4], l[4];
+            for (int j = 0; j < 4; ++j) fix |= split3(v[j], h[j], m[j], l[j]);
             for (int j = 0; j < 4 && k0 + j < K; ++j) {
                 dst[x3_index(k0 + j, 0)] = h[j];
                 dst[x3_index(k0 + j, 1)] = m[j];
@@ -567,16 +582,22 @@ hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int
 // leave more than half of the 256 CUs idle, then 128 x 128 (4 waves).
 bool mfma_big_tiles(int M, int N) { return (long long)((M + 255) / 256) * ((N + 255) / 256) >= 128; }
 
-// Workgroups of the unsplit grid: 128 x 512 tiles, or 128 x 128 ones.
+// M <= 64 on a small grid: 64 x 256 tiles of 4 waves (1 x 4, 64 x 64 each),
+// so no MFMA work and no A staging go to rows past M (the 128 x 128 tiles
+// would spend half of both on copies of row M - 1).
+bool mfma_narrow_tiles(int M, int N) { return M <= 64 && !mfma_big_tiles(M, N); }
+
+// Workgroups of the unsplit grid: 128 x 512 tiles, 64 x 256 or 128 x 128.
 long long mfma_tiles(int M, int N) {
-    return mfma_big_tiles(M, N) ? (long long)((M + 127) / 128) * ((N + 511) / 512)
-                                : (long long)((M + 127) / 128) * ((N + 127) / 128);
+    if (mfma_big_tiles(M, N)) return (long long)((M + 127) / 128) * ((N + 511) / 512);
+    if (mfma_narrow_tiles(M, N)) return (long long)((M + 63) / 64) * ((N + 255) / 256);
+    return (long long)((M + 127) / 128) * ((N + 127) / 128);
 }
 
 // Split-K of a grid with fewer tiles than it can run at once: enough slices
-// of the 64-k blocks to bring it to ~512 workgroups of the small tiles (two
-// fit a CU: 64 KiB of LDS, 4 waves each) or ~256 of the large ones (one per
-// CU), each slice at least 8 blocks, at most 16 slices (k_reduce4's limit);
+// of the 64-k blocks to bring it to ~512 workgroups of the small or narrow
+// tiles (two fit a CU: 64 / 80 KiB of LDS, 4 waves each) or ~256 of the
+// large ones (one per CU), each slice at least 8 blocks, at most 16 slices (k_reduce4's limit);
 // normalized so no slice is empty.  Measured (tools/crossover.py, K = N =
 // 8192): M = 64 0.199 -> 0.062 ms, M = 256 0.212 -> 0.108, M = 1024 (large
 // tiles, 2 slices) 0.456 -> 0.32; targets of 768 / 1024 small tiles or 512
@@ -621,6 +642,14 @@ static hipError_t launch_gemm3_t(const uint16_t* x3, int ldk, const uint16_t* wt
         else
             hipLaunchKernelGGL((k_gemm3<1, 8, 8, 4, false, true>), dim3(tm * tn, slices), dim3(512), 0, st, x3, wt,
                                ldk, ldw, M, N, nblk, nullptr, slabs, N, 0.0f, tm, tn, gm, (nblk + slices - 1) / slices);
+    } else if (mfma_narrow_tiles(M, N)) {
+        const int tn = (N + 255) / 256;
+        if (slices <= 1)
+            hipLaunchKernelGGL((k_gemm3<1, 4, 4, 4, PRELU, false>), dim3(tn), dim3(256), 0, st, x3, wt, ldk, ldw, M, N,
+                               nblk, B, Y, ldy, a, 1, tn, 1, nblk);
+        else
+            hipLaunchKernelGGL((k_gemm3<1, 4, 4, 4, false, true>), dim3(tn, slices), dim3(256), 0, st, x3, wt, ldk, ldw,
+                               M, N, nblk, nullptr, slabs, N, 0.0f, 1, tn, 1, (nblk + slices - 1) / slices);
     } else {
         const int tm = (M + 127) / 128, tn = (N + 127) / 128;
         const int gm = std::min(kGm, tm);

@@ -1,6 +1,6 @@
 """Seeded random shapes across every launch path: the small-M path (M <= 4),
 the gather with and without split-K, the MFMA path (density >= 0.055 with
-M >= 64, where the per-launch cost model picks it; K split over small
+M >= 5, where the per-launch cost model picks it; K split over small
 grids), column blocks with a row
 pitch, all five variants.  Float inputs within the fp32 bound of the exact
 sums, integer inputs bit-exact with the reference's own order (the oracle

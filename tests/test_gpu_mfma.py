@@ -1,7 +1,7 @@
 """The MFMA path for near-dense W (csrc/tcsc_mfma.hip).
 
 Plans of W with density >= 0.055 also hold W as bf16, and launches with
-M >= 64 where the per-launch cost model picks it run Y = [h|m|l] . [W;W;W]
+M >= 5 where the per-launch cost model picks it run Y = [h|m|l] . [W;W;W]
 on the matrix cores (x = h + m + l split exactly into bf16 parts).  At the
 small shapes most tests use the cost model prefers the gather, so they force
 the path (TCSC_PATH=mfma) and check the launch took it; grids of few
@@ -180,12 +180,12 @@ def test_path_modes_and_small_M(gpu, oracle, path):
         Y64, S64 = oracle.f64_rows(X[:M], Wref, B)
         assert pyoracle.check_close(Y, Y64, S64, 0.2)[0]
     W.free()
-    # dense W, M below the threshold: the gather serves it
+    # dense W, M below the threshold (M <= 4): the small-M path serves it
     path(None)
-    Wd2, X2, B2 = float_case(oracle, 40, 300, 128, 0.6, 62)
+    Wd2, X2, B2 = float_case(oracle, 4, 300, 128, 0.6, 62)
     W2 = tcsc_amd.TcscMatrix.from_dense(Wd2)
     Y, info = device_run(W2, X2, B2, "basic")
-    assert info["mfma_min_M"] == 64 and info["launch"][0] == "gather"
+    assert info["mfma_min_M"] == 5 and info["launch"][0] == "small"
     Y64, S64 = oracle.f64_rows(X2, oracle.tcsc_from_dense(Wd2), B2)
     assert pyoracle.check_close(Y, Y64, S64)[0]
     W2.free()
@@ -252,7 +252,7 @@ def test_baseline_cfg5_sampled_rows(gpu, oracle, path):
     tcsc_amd.gpu_from_dense(inp["Wd"], K, N, csp, csn, rip, rin)
     del inp["Wd"]
     plan = tcsc_amd.Plan.from_device(K, N, csp, csn, rip, rin)
-    assert plan.info()["mfma_min_M"] == 64
+    assert plan.info()["mfma_min_M"] == 5
     Y = torch.empty((cfg.M, N), device=dev)
     plan.sgemm(inp["X"], inp["B"], Y, cfg.M, N, "basic", 0.2)
     torch.cuda.synchronize()
@@ -291,11 +291,12 @@ def test_golden_fixtures_forced_mfma(gpu, oracle, path, name):
     W.free()
 
 
-SPLIT_CASES = [  # (M, K, N): grids of few 128 x 128 tiles, so K is split
-    (64, 4096, 300),    # 3 tiles: 8 slices of 8 blocks
-    (256, 4096, 300),   # 6 tiles: 8 slices
+SPLIT_CASES = [  # (M, K, N): grids of few tiles, so K is split
+    (64, 4096, 300),    # 64 x 256 tiles (M <= 64), 2 of them: 8 slices of 8 blocks
+    (256, 4096, 300),   # 128 x 128 tiles, 6: 8 slices
     (100, 2050, 1000),  # 8 tiles: 4 slices of 9, 9, 9, 6 blocks (a ragged last block)
     (130, 1024, 257),   # 9 tiles, ragged row and column tiles: 2 slices
+    (33, 2050, 700),    # 64 x 256 tiles, 3, a ragged row tile: 4 slices
 ]
 
 
@@ -317,6 +318,29 @@ def test_split_k_integer_exact_all_variants(gpu, oracle, path, case):
         np.testing.assert_array_equal(Y.view(np.uint32), ref.view(np.uint32), err_msg=variant)
     Yh = tcsc_amd.sgemm("prelu_onthego", X, W, B, 0.2)
     np.testing.assert_array_equal(Yh, oracle.sgemm("prelu_onthego", X, Wref, B, 0.2))
+    W.free()
+
+
+@pytest.mark.parametrize("M", [5, 17, 64])
+def test_narrow_tiles_unsplit_and_split_integer_exact(gpu, oracle, path, monkeypatch, M):
+    """M <= 64 runs 64 x 256 tiles; unsplit ($TCSC_MFMA_WGS=0) and split,
+    integer inputs bit for bit against the reference's outputs (ragged N)."""
+    path("mfma")
+    K, N = 1500, 520
+    Wd = oracle.ternary((K, N), 0.4, 780 + M)
+    X, B = oracle.integers((M, K), 781 + M), oracle.integers((N,), 782 + M)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    Wref = oracle.tcsc_from_dense(Wd)
+    for wgs, split in (("0", False), (None, True)):
+        if wgs is None:
+            monkeypatch.delenv("TCSC_MFMA_WGS", raising=False)
+        else:
+            monkeypatch.setenv("TCSC_MFMA_WGS", wgs)
+        for variant in ("basic", "prelu_separate"):
+            Y, info = device_run(W, X, B, variant)
+            assert info["launch"][0] == "mfma" and (info["launch"][1] > 1) == split, info["launch"]
+            ref = oracle.sgemm(variant, X, Wref, B, 0.2)
+            np.testing.assert_array_equal(Y.view(np.uint32), ref.view(np.uint32), err_msg=f"{variant} wgs={wgs}")
     W.free()
 
 
@@ -396,7 +420,7 @@ def test_cost_model_takes_the_split_gemm(gpu, oracle, path):
     Wd, X, B = float_case(oracle, M, K, N, 0.5, 751)
     W = tcsc_amd.TcscMatrix.from_dense(Wd)
     Y, info = device_run(W, X, B, "basic")
-    assert info["mfma_min_M"] == 64 and info["launch"] == ("mfma", 4), info["launch"]
+    assert info["mfma_min_M"] == 5 and info["launch"] == ("mfma", 4), info["launch"]
     rows = np.arange(0, M, 17)
     Y64, S64 = oracle.f64_rows(X[rows], oracle.tcsc_from_dense(Wd), B)
     ok, ratio = pyoracle.check_close(Y[rows], Y64, S64)
