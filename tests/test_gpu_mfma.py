@@ -431,7 +431,7 @@ def test_cost_model_takes_the_split_gemm(gpu, oracle, path):
 def test_reference_order_never_takes_the_mfma_path(gpu, oracle, path):
     """TCSC_ORDER_REFERENCE plans keep the gather (the reference's order is a
     sequence of fp32 adds a GEMM cannot reproduce): a near-dense W with
-    M >= 64 stays bit-identical to the oracle's restatement of tcsc.c."""
+    M >= 5 stays bit-identical to the oracle's restatement of tcsc.c."""
     path(None)
     Wd, X, B = float_case(oracle, 128, 300, 96, 0.5, 101)
     W = tcsc_amd.TcscMatrix.from_dense(Wd)
