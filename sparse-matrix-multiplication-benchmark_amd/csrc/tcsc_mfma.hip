@@ -596,23 +596,26 @@ long long mfma_tiles(int M, int N) {
 
 // Split-K of a grid with fewer tiles than it can run at once: enough slices
 // of the 64-k blocks to bring it to ~512 workgroups of the small or narrow
-// tiles (two fit a CU: 64 / 80 KiB of LDS, 4 waves each) or ~256 of the
+// tiles (two fit a CU: 64 / 80 KiB of LDS, 4 waves each; ~1,024 of the
+// narrow ones, whose slices are cheap to reduce: M <= 64) or ~256 of the
 // large ones (one per CU), each slice at least 8 blocks, at most 16 slices (k_reduce4's limit);
 // normalized so no slice is empty.  Measured (tools/crossover.py, K = N =
 // 8192): M = 64 0.199 -> 0.062 ms, M = 256 0.212 -> 0.108, M = 1024 (large
 // tiles, 2 slices) 0.456 -> 0.32; targets of 768 / 1024 small tiles or 512
-// large ones were slower.  $TCSC_MFMA_WGS overrides the target (A/B; 0 =
+// large ones were slower.  Narrow tiles: 1024 equals 512 at K = N = 8192 (16
+// slices either way) and is 19 % faster at M = 16, K = N = 16384.  $TCSC_MFMA_WGS overrides the target (A/B; 0 =
 // never split).
-int mfma_split_target(bool big) {
+int mfma_split_target(bool big, bool narrow) {
     const char* e = std::getenv("TCSC_MFMA_WGS");
-    return e ? std::atoi(e) : big ? 256 : 512;
+    return e ? std::atoi(e) : big ? 256 : narrow ? 1024 : 512;
 }
 
 int mfma_slices(int M, int N, int K) {
     if (M <= 0 || N <= 0) return 1;
     const long long tiles = mfma_tiles(M, N);
     const int nblk = mfma_nblk(K);
-    const long long s = std::min<long long>({mfma_split_target(mfma_big_tiles(M, N)) / tiles, 16, nblk / 8});
+    const long long s =
+        std::min<long long>({mfma_split_target(mfma_big_tiles(M, N), mfma_narrow_tiles(M, N)) / tiles, 16, nblk / 8});
     if (s < 2) return 1;
     const int bps = (int)((nblk + s - 1) / s);
     return (nblk + bps - 1) / bps;
