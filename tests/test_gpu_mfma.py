@@ -363,12 +363,14 @@ def test_split_k_big_tiles_sampled_rows_integer_exact(gpu, oracle, path):
     W.free()
 
 
-def test_split_k_float_blocks_pitch_prepared(gpu, oracle, path, monkeypatch):
-    """Float inputs through the split GEMM: column blocks (N % 4 != 0 takes
-    k_reduce's scalar form), a row pitch past N, prepare_x + sgemm_prepared;
-    within the fp32 bound, and the unsplit GEMM ($TCSC_MFMA_WGS=0) too."""
+@pytest.mark.parametrize("M", [96, 40])
+def test_split_k_float_blocks_pitch_prepared(gpu, oracle, path, monkeypatch, M):
+    """Float inputs through the split GEMM (128 x 128 tiles at M = 96, 64 x 256
+    at M = 40): column blocks (N % 4 != 0 takes k_reduce's scalar form), a row
+    pitch past N, prepare_x + sgemm_prepared; within the fp32 bound, and the
+    unsplit GEMM ($TCSC_MFMA_WGS=0) too."""
     path("mfma")
-    M, K, N = 96, 3000, 600
+    K, N = 3000, 600
     Wd, X, B = float_case(oracle, M, K, N, 0.4, 731)
     W = tcsc_amd.TcscMatrix.from_dense(Wd)
     Y64, S64 = oracle.f64_rows(X, oracle.tcsc_from_dense(Wd), B)
@@ -409,6 +411,32 @@ def test_split_k_special_rows_match_the_gather(gpu, oracle, path, monkeypatch):
     rest = np.setdiff1d(np.arange(M), flagged)
     Y64, S64 = oracle.f64_rows(X[rest], oracle.tcsc_from_dense(Wd), B)
     assert pyoracle.check_close(Ym[rest], Y64, S64, 0.2)[0]
+    W.free()
+
+
+@pytest.mark.parametrize("axis", ["cols", "rows"])
+def test_host_fast_mode_small_m_shards(gpu, oracle, path, monkeypatch, axis):
+    """The host API in fast mode ($TCSC_HOST_FAST=1) at M = 40 over 3 blocks
+    of either axis (the cost model sends each block to the GEMM's 64 x 256
+    tiles with K split); within the fp32 bound.  The default exact mode gives gemm_basic's
+    bits on the same call."""
+    path(None)
+    monkeypatch.setenv("TCSC_SHARD_AXIS", axis)
+    M, K, N = 40, 2048, 900
+    Wd, X, B = float_case(oracle, M, K, N, 0.3, 771)
+    W = tcsc_amd.TcscMatrix.from_dense(Wd)
+    Y64, S64 = oracle.f64_rows(X, oracle.tcsc_from_dense(Wd), B)
+    tcsc_amd.set_num_shards(3)
+    try:
+        Y = tcsc_amd.sgemm("prelu_basic", X, W, B, 0.2)
+        ok, ratio = pyoracle.check_close(Y, Y64, S64, 0.2)
+        assert ok, ratio
+        monkeypatch.delenv("TCSC_HOST_FAST")
+        Ye = tcsc_amd.sgemm("prelu_basic", X, W, B, 0.2)
+        want = pyoracle.prelu(oracle.gemm_basic(X, Wd, B), 0.2)
+        np.testing.assert_array_equal(Ye.view(np.uint32), want.view(np.uint32))
+    finally:
+        tcsc_amd.set_num_shards(0)
     W.free()
 
 
