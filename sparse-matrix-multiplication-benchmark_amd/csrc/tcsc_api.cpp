@@ -627,9 +627,11 @@ int sgemm_mfma(const tcsc_gpu_plan* p, const float* dX, const float* dB, float* 
     if (stage == 1) return TCSC_OK;
     const bool prelu = is_prelu(variant);
     HIP_TRY(tcsc::mfma_gemm3(x3, ldk, p->wt, tcsc::mfma_ldw(K), K, M, N, dB, dY, ldy, prelu, a, slabs,
-                             ws_bytes - mfma_slabs_off(M, K), st));
-    // fast order: bias after the sum for every variant
-    HIP_TRY(tcsc::mfma_fixup(x3, M, K, ldk, p->ccq, p->crq, N, dB, dY, ldy, false, prelu, a, flags, st));
+                             ws_bytes - mfma_slabs_off(M, K), flags, p->ccq, p->crq, st));
+    // fast order: bias after the sum for every variant; a
+    // split K rewrote the flagged rows in its reduce already
+    if (tcsc::mfma_slices(M, N, K) <= 1)
+        HIP_TRY(tcsc::mfma_fixup(x3, M, K, ldk, p->ccq, p->crq, N, dB, dY, ldy, false, prelu, a, flags, st));
     return TCSC_OK;
 }
 

@@ -328,18 +328,18 @@ hipError_t mfma_split_x(const float* X, int M, int K, uint16_t* x3, int ldk, int
 // cores (bias after the sum); K gives the block count.  Grids of small tiles
 // that would leave CUs idle split K into mfma_slices() slices of whole 64-k
 // blocks: raw partial sums into `slabs` (mfma_slab_bytes(): slices x M x N
-// floats), added in slice order with the bias and PReLU by k_reduce4.
+// floats), added in slice order with the bias and PReLU (k_reduce4's adds)
+// by k_reduce_fix, which also writes the rows `flags` marks exactly (the
+// fixup, from the CSC copy cq / crq): a split call needs no mfma_fixup.
 bool mfma_big_tiles(int M, int N);
 bool mfma_narrow_tiles(int M, int N);
 long long mfma_tiles(int M, int N);
 int mfma_slices(int M, int N, int K);
 size_t mfma_slab_bytes(int M, int N, int K);
 hipError_t mfma_gemm3(const uint16_t* x3, int ldk, const uint16_t* wt, int ldw, int K, int M, int N, const float* B,
-                      float* Y, int ldy, bool prelu, float a, float* slabs, size_t slab_bytes, hipStream_t st);
-// Y = act(b + s0 + s1 + ...) (bias_first) or act(s0 + s1 + ... + b) over
-// `slices` fp32 slabs of M x ncols (pitch ncols), in slice order.
-hipError_t launch_reduce_slabs(const float* ws, int slices, int M, int ncols, const float* B, float* Y, int ldy,
-                               bool bias_first, bool prelu, float a, hipStream_t st);
+                      float* Y, int ldy, bool prelu, float a, float* slabs, size_t slab_bytes, const int* flags,
+                      const int* cq, const int* crq, hipStream_t st);
+
 // Rewrites the flagged rows in k_stream's fast order (no-op when none is).
 hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cq, const int* crq, int ncols,
                       const float* B, float* Y, int ldy, bool bias_first, bool prelu, float a, const int* flags,

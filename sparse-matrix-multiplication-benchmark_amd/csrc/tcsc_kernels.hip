@@ -1645,34 +1645,6 @@ hipError_t dense_to_tcsc_fill(const float* D, int rows, int cols, const int* csp
     return hipGetLastError();
 }
 
-template <bool BF, bool PR>
-static void reduce_slabs_t(const float* ws, int slices, int M, int ncols, const float* B, float* Y, int ldy, float a,
-                           hipStream_t st) {
-    const long long total = (long long)M * ncols;
-    const bool vec = slices <= 16 && ncols % 4 == 0 && ldy % 4 == 0 &&
-                     ((reinterpret_cast<uintptr_t>(Y) | reinterpret_cast<uintptr_t>(ws) |
-                       reinterpret_cast<uintptr_t>(B)) & 15) == 0;
-    if (vec)
-        hipLaunchKernelGGL((k_reduce4<BF, PR>), dim3(grid_for(total / 4, 256)), dim3(256), 0, st,
-                           reinterpret_cast<const f32x4_t*>(ws), slices, M, ncols, B, Y, ldy, a);
-    else
-        hipLaunchKernelGGL((k_reduce<BF, PR>), dim3(grid_for(total, 256)), dim3(256), 0, st, ws, slices, M, ncols, B,
-                           Y, ldy, a);
-}
-
-hipError_t launch_reduce_slabs(const float* ws, int slices, int M, int ncols, const float* B, float* Y, int ldy,
-                               bool bias_first, bool prelu, float a, hipStream_t st) {
-    if (M <= 0 || ncols <= 0) return hipSuccess;
-    if (bias_first) {
-        if (prelu) reduce_slabs_t<true, true>(ws, slices, M, ncols, B, Y, ldy, a, st);
-        else reduce_slabs_t<true, false>(ws, slices, M, ncols, B, Y, ldy, a, st);
-    } else {
-        if (prelu) reduce_slabs_t<false, true>(ws, slices, M, ncols, B, Y, ldy, a, st);
-        else reduce_slabs_t<false, false>(ws, slices, M, ncols, B, Y, ldy, a, st);
-    }
-    return hipGetLastError();
-}
-
 hipError_t launch_bias_act(float* Y, int M, int N, int ldy, const float* B, bool prelu, float a, hipStream_t st) {
     const long long total = (long long)M * ((N + 3) / 4);
     if (total == 0) return hipSuccess;

@@ -279,6 +279,63 @@ __global__ void __launch_bounds__(256) k_fixup(const uint16_t* __restrict__ X3, 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Split K (k_gemm3 PARTIAL): the slabs added in slice order, then the bias,
+// then the PReLU -- k_reduce4's arithmetic, element for element -- with
+// k_fixup folded in: a flagged row takes exact_out() instead, so a split call
+// needs no fixup launch.  VEC: 4 columns per thread (N % 4 == 0, ldy % 4 ==
+// 0, 16-B aligned slabs, bias and Y), all slices' loads in flight.
+template <bool PRELU, bool VEC>
+__global__ void __launch_bounds__(256) k_reduce_fix(const float* __restrict__ ws, int slices, int M, int N,
+                                                    const float* __restrict__ Bias, float* __restrict__ Y, int ldy,
+                                                    float a, const int* __restrict__ flags,
+                                                    const uint16_t* __restrict__ X3, int K, int ldk,
+                                                    const int* __restrict__ cq, const int* __restrict__ rm) {
+    constexpr int W = VEC ? 4 : 1;
+    const int nq = N / W;
+    const long long total = (long long)M * nq;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int row = (int)(i / nq), col = W * (int)(i % nq);
+        float v[W];
+        if (flags[row]) {
+#pragma unroll
+            for (int u = 0; u < W; ++u) v[u] = exact_out<false, PRELU>(X3, K, ldk, cq, rm, Bias, row, col + u, a);
+        } else {
+            const size_t slab = (size_t)M * N, e = (size_t)row * N + col;
+            float p[16][W];
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+                if (s < slices) {
+                    if constexpr (VEC) {
+                        const f32x4 q = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ws + s * slab + e));
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) p[s][u] = q[u];
+                    } else {
+                        p[s][0] = ws[s * slab + e];
+                    }
+                }
+#pragma unroll
+            for (int u = 0; u < W; ++u) {
+                float t = 0.f;
+#pragma unroll
+                for (int s = 0; s < 16; ++s)
+                    if (s < slices) t += p[s][u];
+                t += Bias[col + u];
+                if (PRELU) t = (t < 0.0f) ? a * t : t;
+                v[u] = t;
+            }
+        }
+        float* dst = Y + (size_t)row * ldy + col;
+        if constexpr (VEC) {
+            const f32x4 o = {v[0], v[1], v[2], v[3]};
+            __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(dst));
+        } else {
+            dst[0] = v[0];
+        }
+    }
+}
+
+
 // XCD-aware bijective renumbering of blockIdx.x (an XCD's workgroups get
 // consecutive numbers), then bands of gm row tiles walked column by column:
 // an XCD's ~32 concurrent workgroups take gm row tiles x 32 / gm column
@@ -627,9 +684,9 @@ size_t mfma_slab_bytes(int M, int N, int K) {
 }
 
 template <bool PRELU>
-static hipError_t launch_gemm3_t(const uint16_t* x3, int ldk, const uint16_t* wt, int ldw, int nblk, int M, int N,
-                                 const float* B, float* Y, int ldy, float a, float* slabs, int slices,
-                                 hipStream_t st) {
+static hipError_t launch_gemm3_t(const uint16_t* x3, int ldk, const uint16_t* wt, int ldw, int K, int nblk, int M,
+                                 int N, const float* B, float* Y, int ldy, float a, float* slabs, int slices,
+                                 const int* flags, const int* cq, const int* crq, hipStream_t st) {
     // bands of 4 row tiles: an XCD's 32 workgroups share 4 A tiles (staged every
     // sub-step) and 8 W tiles (once per block); 8 x 4 was 2 % slower at cfg 5
     constexpr int kGm = 4;
@@ -664,21 +721,34 @@ static hipError_t launch_gemm3_t(const uint16_t* x3, int ldk, const uint16_t* wt
                                ldk, ldw, M, N, nblk, nullptr, slabs, N, 0.0f, tm, tn, gm, (nblk + slices - 1) / slices);
     }
     // split K: raw partial tiles went into slabs[slice] (M x N); then
-    // act(s0 + s1 + ... + b) in slice order by k_reduce4
+    // act(s0 + s1 + ... + b) in slice order, flagged rows exact (k_fixup's)
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess || slices <= 1) return e;
-    return launch_reduce_slabs(slabs, slices, M, N, B, Y, ldy, false, PRELU, a, st);
+    const bool vec = N % 4 == 0 && ldy % 4 == 0 &&
+                     ((reinterpret_cast<uintptr_t>(Y) | reinterpret_cast<uintptr_t>(slabs) |
+                       reinterpret_cast<uintptr_t>(B)) & 15) == 0;
+    const long long n = (long long)M * (vec ? N / 4 : N);
+    if (vec)
+        hipLaunchKernelGGL((k_reduce_fix<PRELU, true>), dim3(grid_of(n, 256)), dim3(256), 0, st, slabs, slices, M, N, B,
+                           Y, ldy, a, flags, x3, K, ldk, cq, crq);
+    else
+        hipLaunchKernelGGL((k_reduce_fix<PRELU, false>), dim3(grid_of(n, 256)), dim3(256), 0, st, slabs, slices, M, N,
+                           B, Y, ldy, a, flags, x3, K, ldk, cq, crq);
+    return hipGetLastError();
 }
 
 hipError_t mfma_gemm3(const uint16_t* x3, int ldk, const uint16_t* wt, int ldw, int K, int M, int N, const float* B,
-                      float* Y, int ldy, bool prelu, float a, float* slabs, size_t slab_bytes, hipStream_t st) {
+                      float* Y, int ldy, bool prelu, float a, float* slabs, size_t slab_bytes, const int* flags,
+                      const int* cq, const int* crq, hipStream_t st) {
     if (M <= 0 || N <= 0) return hipSuccess;
     const int nblk = mfma_nblk(K);
     if (nblk < 1 || ldk != mfma_ldk(K) || ldw != mfma_ldw(K)) return hipErrorInvalidValue;
     const int slices = mfma_slices(M, N, K);
     if (slices > 1 && (!slabs || slab_bytes < mfma_slab_bytes(M, N, K))) return hipErrorInvalidValue;
-    return prelu ? launch_gemm3_t<true>(x3, ldk, wt, ldw, nblk, M, N, B, Y, ldy, a, slabs, slices, st)
-                 : launch_gemm3_t<false>(x3, ldk, wt, ldw, nblk, M, N, B, Y, ldy, a, slabs, slices, st);
+    return prelu ? launch_gemm3_t<true>(x3, ldk, wt, ldw, K, nblk, M, N, B, Y, ldy, a, slabs, slices, flags, cq, crq,
+                                        st)
+                 : launch_gemm3_t<false>(x3, ldk, wt, ldw, K, nblk, M, N, B, Y, ldy, a, slabs, slices, flags, cq, crq,
+                                         st);
 }
 
 hipError_t mfma_fixup(const uint16_t* x3, int M, int K, int ldk, const int* cq, const int* crq, int ncols,

@@ -389,11 +389,13 @@ def test_split_k_float_blocks_pitch_prepared(gpu, oracle, path, monkeypatch, M):
     W.free()
 
 
-def test_split_k_special_rows_match_the_gather(gpu, oracle, path, monkeypatch):
-    """Rows the bf16 split cannot carry are rewritten by k_fixup after the
-    slabs are reduced: bit-identical to the unsplit gather."""
+@pytest.mark.parametrize("N", [200, 203])
+def test_split_k_special_rows_match_the_gather(gpu, oracle, path, monkeypatch, N):
+    """Rows the bf16 split cannot carry are written exactly by the split's
+    reduce (k_reduce_fix, the fixup folded in; 4 columns per thread at
+    N = 200, one at 203): bit-identical to the unsplit gather."""
     monkeypatch.setenv("TCSC_SLICES", "1")
-    M, K, N = 70, 2048, 200
+    M, K = 70, 2048
     Wd, X, B = float_case(oracle, M, K, N, 0.3, 741)
     X[5, 1000] = np.inf
     X[6, 7] = np.nan
