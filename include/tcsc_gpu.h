@@ -116,8 +116,9 @@ int tcsc_gpu_plan_get_info(const tcsc_gpu_plan *plan, tcsc_gpu_plan_info *info);
  * aligned, the plan's reserved workspace and the current environment):
  *   TCSC_PATH_GATHER k_transpose + k_stream (+ k_reduce, or the in-launch
  *                    combine: tcsc_gpu_launch_combine)
- *   TCSC_PATH_MFMA   k_split3 + k_gemm3 (+ k_reduce4 when K is split,
- *                    + k_fixup), denser W (the cost model)
+ *   TCSC_PATH_MFMA   k_split3 + k_gemm3 + k_fixup, or with K split
+ *                    k_split3 + k_gemm3 + k_reduce_fix (the slabs and the
+ *                    fixup in one kernel), denser W (the cost model)
  *   TCSC_PATH_SMALL  k_small_m, M <= 4 (X and -X fit the LDS)
  * and *slices = the K split (1 = none): the gather's, or the MFMA GEMM's on
  * grids of few 128 x 128 tiles (M <= 256 at N = 8192: partial sums of whole
@@ -177,7 +178,7 @@ void tcsc_gpu_plan_destroy(tcsc_gpu_plan *plan);
  * accumulation against the plan's bf16 image of W on the matrix cores
  * (k_gemm3, the library's own gfx950 kernel, bias and PReLU fused in its
  * store; a grid with fewer tiles than the chip runs at once splits K into
- * slices of whole 64-k blocks whose partial sums k_reduce4 adds in slice
+ * slices of whole 64-k blocks whose partial sums k_reduce_fix adds in slice
  * order with the bias and PReLU), then the exact fixup of
  * rows holding non-finite or tiny values (k_fixup) -- with the same accuracy
  * bounds as the gather.  It allocates nothing per launch and
